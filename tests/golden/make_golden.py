@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ (container only).
+
+Runs oracle/_ref/ref_harness -- the real reference compiled from
+/root/reference by `make -C oracle ref` -- and converts its record files into
+small .npz fixtures.  Re-run after changing the harness:
+
+    make -C oracle ref && python tests/golden/make_golden.py
+
+The fixtures are data only (inputs and expected outputs).  Each entry in
+FIXTURES says which reference code path produced it.
+"""
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+REF = "/root/reference"
+
+_DT = {b"f": np.float32, b"d": np.float64, b"i": np.int32, b"u": np.uint32}
+
+
+def read_records(path):
+    out = {}
+    with open(path, "rb") as f:
+        data = f.read()
+    off = 0
+    while off < len(data):
+        (nl,) = struct.unpack_from("<I", data, off)
+        off += 4
+        name = data[off:off + nl].decode()
+        off += nl
+        dt = data[off:off + 1]
+        off += 1
+        (nd,) = struct.unpack_from("<I", data, off)
+        off += 4
+        dims = struct.unpack_from("<%dQ" % nd, data, off)
+        off += 8 * nd
+        dtype = np.dtype(_DT[dt])
+        n = int(np.prod(dims)) if nd else 1
+        arr = np.frombuffer(data, dtype=dtype, count=n, offset=off).reshape(dims)
+        off += n * dtype.itemsize
+        out[name] = arr.copy()
+    return out
+
+
+# name -> (harness mode, args, small-ification)
+FIXTURES = {
+    # minstd_rand0 / generate_canonical / bernoulli / discrete_distribution
+    # (xylo/tensor.cc:71-75, 467-470; apps/bin_packing/bin_packing.h:81)
+    "rng": ("rng", ["seed=42", "n=8000"]),
+    # bp::environment + bp::agent + random_policy (bin_packing.h:46-107,
+    # rl.h:305-349), and gen_env<8,2> equivalence
+    "env8": ("envcheck", ["seed=7", "steps=3000"]),
+    # deep_agent.cc with weights.20, seed 1, 1000 argmax episodes
+    "deep_w20": ("deep", ["seed=1", "episodes=1000",
+                          "weights=%s/apps/bin_packing/weights.20" % REF]),
+    # ppo_training.cc shapes: conv 4->128->64->1 + softmax, value 32->64->32->1
+    "ppo_b8d2": ("learn", ["algo=ppo", "B=8", "D=2", "widths=128,64", "N=8",
+                           "T=8", "iters=5", "seed=42"]),
+    # BASELINE config 2 shape (1-D, 32 bins, [64,64])
+    "ppo_b32d1": ("learn", ["algo=ppo", "B=32", "D=1", "widths=64,64", "N=6",
+                            "T=4", "iters=2", "seed=5"]),
+    # BASELINE config 3/4 shape (2-D, 64 bins, [128,128])
+    "ppo_b64d2": ("learn", ["algo=ppo", "B=64", "D=2", "widths=128,128",
+                            "N=4", "T=4", "iters=2", "seed=11"]),
+    # ac_training.cc shapes: conv 4->64->32->1 + softmax-xent, 16x8
+    "ac_b8d2": ("learn", ["algo=ac", "B=8", "D=2", "widths=64,32", "N=16",
+                          "T=8", "iters=4", "seed=3"]),
+    # BASELINE config 5 shape (3-D, 128 bins, [128,128], actor-critic)
+    "ac_b128d3": ("learn", ["algo=ac", "B=128", "D=3", "widths=128,128",
+                            "N=2", "T=8", "iters=2", "seed=13"]),
+    # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])
+    "pg_b8d1": ("learn", ["algo=pg", "B=8", "D=1", "widths=32", "N=1",
+                          "episodes=4", "iters=3", "seed=17"]),
+}
+
+
+def main(names):
+    if not os.path.exists(HARNESS):
+        sys.exit("build the harness first: make -C oracle ref")
+    names = names or list(FIXTURES)
+    for name in names:
+        mode, args = FIXTURES[name]
+        with tempfile.TemporaryDirectory() as td:
+            rec = os.path.join(td, "out.rec")
+            subprocess.run([HARNESS, mode, "out=" + rec] + args, check=True,
+                           cwd=td)
+            arrs = read_records(rec)
+        meta = {"mode": mode, "args": " ".join(args)}
+        for k, v in meta.items():
+            arrs["meta_" + k] = np.array(v)
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **arrs)
+        print("%-10s %8d bytes  %d arrays" % (name, os.path.getsize(path),
+                                                len(arrs)))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,170 @@
+"""Pin the CPU oracle (oracle/oracle.c) to the real reference's golden vectors.
+
+The golden .npz fixtures were produced by oracle/_ref/ref_harness -- the
+reference compiled from /root/reference with its own flags -- via
+tests/golden/make_golden.py.  CPU only.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_close, golden
+from oracle import pyoracle as po
+
+
+def parse_meta(d):
+    kv = dict(a.split("=", 1) for a in str(d["meta_args"]).split())
+    return kv
+
+
+def models_for(kv):
+    B, D = int(kv["B"]), int(kv["D"])
+    widths = [int(w) for w in kv["widths"].split(",")]
+    algo = kv["algo"]
+    if algo == "pg":
+        pol = po.full_model(B * 2 * D, widths, B, po.OR_SOFTMAX_XENT)
+        return pol, None
+    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    pol = po.perbin_model(2 * D, widths, head)
+    val = po.full_model(B * 2 * D, [64, 32], 1)
+    return pol, val
+
+
+# ------------------------------------------------------------------ RNG ----
+def test_minstd_raw_and_canonical():
+    g = golden("rng")
+    r = po.Rng.seeded(42)
+    raw = np.array([r.next() for _ in range(len(g["raw"]))], np.uint32)
+    np.testing.assert_array_equal(raw, g["raw"])
+    r = po.Rng.seeded(42)
+    can = np.array([r.canonical() for _ in range(len(g["canonical"]))])
+    np.testing.assert_array_equal(can, g["canonical"])  # bit-exact doubles
+
+
+def test_bernoulli():
+    g = golden("rng")
+    r = po.Rng.seeded(42)
+    b = np.array([r.bernoulli(0.4) for _ in range(len(g["bernoulli"]))])
+    np.testing.assert_array_equal(b, g["bernoulli"])
+
+
+@pytest.mark.parametrize("width", [8, 32, 64, 128])
+def test_discrete_distribution(width):
+    g = golden("rng")
+    probs, picks = g["disc_probs_%d" % width], g["disc_pick_%d" % width]
+    r = po.Rng.seeded(42 + width)
+    got = np.array([r.discrete(p) for p in probs])
+    np.testing.assert_array_equal(got, picks)
+    assert r.state == int(g["disc_state_after_%d" % width][0])
+
+
+def test_jump_ahead():
+    r = po.Rng.seeded(123)
+    for _ in range(1000):
+        r.next()
+    assert po.minstd_jump(po.lib().or_minstd_seed(123), 1000) == r.state
+
+
+# ------------------------------------------------------------------ env ----
+def test_env_trajectory_bit_exact():
+    """bp::environment + bp::agent + random_policy, 3000 steps, seed 7."""
+    g = golden("env8")
+    cfg = po.env_cfg(8, 2)
+    rng = po.Rng(int(g["x0"][0]))
+    env = po.Env(cfg, rng)
+    uniform = np.full(8, np.float32(1.0) / np.float32(8), np.float32)
+    n = len(g["choice"])
+    for k in range(n):
+        np.testing.assert_array_equal(env.bins, g["start_bins"][k])
+        np.testing.assert_array_equal(env.item[:2], g["start_item"][k])
+        c = rng.discrete(uniform)
+        assert c == g["choice"][k]
+        env.apply(c)
+        np.testing.assert_array_equal(env.bins, g["end_bins"][k])
+        np.testing.assert_array_equal(env.item[:2], g["end_item"][k])
+        over = bool((env.bins < 0).any())
+        assert int(not over) == g["reward"][k]
+        if over:
+            env.reset()
+    assert rng.state == int(g["x_end"][0])
+    assert int(g["gen_env_identical"][0]) == 1
+
+
+# ---------------------------------------------------------- deep agent ----
+def test_weights20_logits_and_argmax_episodes():
+    g = golden("deep_w20")
+    m = po.perbin_model(4, [128, 64], None)
+    assert po.nparams(m) == 8961 == g["params"].size
+    z = po.model_eval(m, g["params"], g["obs"])
+    assert_close(z, g["logits"], what="weights.20 logits")
+    # empty bins, item (4,2): every bin scores the same
+    assert np.allclose(z[0], z[0, 0])
+    total, _ = po.eval_argmax(8, 2, m, g["params"], 1000, int(g["x0"][0]))
+    assert total == float(g["total_reward"][0]) == 26600.0
+
+
+# ------------------------------------------------------------- learners ----
+LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1"]
+
+
+def run_oracle_against(name, forced=True):
+    g = golden(name)
+    kv = parse_meta(g)
+    B, D, N = int(kv["B"]), int(kv["D"]), int(kv["N"])
+    T = int(kv.get("T", 4))
+    algo = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG}[kv["algo"]]
+    pol, val = models_for(kv)
+    lr_pi = 1e-5 if kv["algo"] == "ac" else 1e-4
+    lr_v = 1e-4 if kv["algo"] == "ac" else 1e-5
+    tr = po.Trainer(algo, B, D, N, T, pol, g["init_policy"], val,
+                    g["init_value"] if val is not None else None, lr_pi=lr_pi,
+                    lr_v=lr_v, gamma=0.99, x0=int(g["x0"][0]),
+                    episodes=int(kv.get("episodes", 1)))
+    iters = int(kv["iters"])
+    worst = {}
+    for it in range(iters):
+        p = "it%d_" % it
+        f = g[p + "step_choice"] if (forced and algo != po.OR_PG) else None
+        tr.rollout(forced=f)
+        ns = len(g[p + "step_choice"])
+        np.testing.assert_array_equal(
+            tr.buf(po.BUF_STEP_BINS).reshape(ns, B, D), g[p + "step_bins"])
+        np.testing.assert_array_equal(
+            tr.buf(po.BUF_STEP_ITEM).reshape(ns, D), g[p + "step_item"])
+        np.testing.assert_array_equal(tr.buf(po.BUF_STEP_CHOICE), g[p + "step_choice"])
+        np.testing.assert_array_equal(tr.buf(po.BUF_STEP_DONE), g[p + "step_done"])
+        pch = g[p + "step_distrib"][np.arange(ns), g[p + "step_choice"]]
+        worst["p_old"] = max(worst.get("p_old", 0),
+                             assert_close(tr.buf(po.BUF_STEP_PCHOICE), pch, what="p_old"))
+        np.testing.assert_array_equal(
+            tr.buf(po.BUF_FINAL_BINS).reshape(N, B, D), g[p + "final_bins"])
+        tr.learn()
+        rows = g[p + "rows"]
+        np.testing.assert_array_equal(tr.buf(po.BUF_ROWS).reshape(rows.shape), rows)
+        np.testing.assert_array_equal(tr.buf(po.BUF_ROW_ENV), g[p + "row_env"])
+        np.testing.assert_array_equal(tr.buf(po.BUF_ROW_STEP), g[p + "row_step"])
+        np.testing.assert_array_equal(tr.buf(po.BUF_ROW_IS_END), g[p + "row_is_end"])
+        checks = [("advantages", tr.buf(po.BUF_ADVANTAGES), g[p + "advantages"]),
+                  ("policy_grads", tr.buf(po.BUF_POLICY_GRADS),
+                   g[p + "policy_grads"].ravel()),
+                  ("policy_params", tr.params(0), g[p + "policy_params"])]
+        if algo != po.OR_PG:
+            checks += [("values", tr.buf(po.BUF_VALUES), g[p + "values_before"]),
+                       ("value_grad", tr.buf(po.BUF_VALUE_GRAD), g[p + "value_grad"]),
+                       ("value_params", tr.params(1), g[p + "value_params"])]
+        for what, x, y in checks:
+            worst[what] = max(worst.get(what, 0), assert_close(x, y, what=p + what))
+        assert tr.rng == int(g[p + "x_end"][0])
+    return worst
+
+
+@pytest.mark.parametrize("name", LEARN)
+def test_learner_matches_reference(name):
+    worst = run_oracle_against(name, forced=True)
+    print(name, {k: "%.2e" % v for k, v in worst.items()})
+
+
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "pg_b8d1"])
+def test_free_running_sampling_matches_reference(name):
+    """Without teacher forcing the oracle's own sampler reproduces the
+    reference's actions (no probability near-ties in these fixtures)."""
+    run_oracle_against(name, forced=False)
