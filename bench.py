@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: PPO env-steps/s on vectorised 64-bin x 2-D bin packing.
+
+BASELINE.json metric "env-steps/sec (whole node) PPO bin-packing 64-bin";
+workload = BASELINE config 3 per GPU (32768 envs, 64 bins, D=2, per-bin
+policy [128,128], value [256,64,32], T=4, k=4 PPO epochs), weak-scaled over
+N GPUs (config 4 at N=8).  A "step" is one training iteration: T env steps
+of every env + learn() (value step, GAE, 4 policy epochs), i.e. N*T env-steps.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  The timed region starts with all state
+resident in HBM; rank 0 additionally times the reference CPU path
+(oracle/_ref, single thread) on a bounded sample: `cpu_baseline`.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+B, D, T, H1, H2, V1, V2 = 64, 2, 4, 128, 128, 64, 32
+F0 = 2 * D
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def policy_fwd_flops_per_env_step():
+    # 2*B*(F0*H1 + H1*H2 + H2): per-bin Dense chain
+    return 2 * B * (F0 * H1 + H1 * H2 + H2)
+
+
+def value_fwd_flops_per_row():
+    fin = B * F0
+    return 2 * (fin * V1 + V1 * V2 + V2)
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """Time the reference's single-threaded CPU path on a bounded sample of
+    the same workload (64 bins, 2-D, [128,128], PPO k=4, T=4)."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    n_env, iters = 16, 20
+    sample = ("reference ppo_learner, %d envs x T=%d x %d iterations, B=64 D=2 "
+              "[128,128], 1 thread" % (n_env, T, iters))
+    if os.path.exists(harness):
+        try:
+            out = subprocess.run(
+                [harness, "bench", "algo=ppo", "B=64", "D=2", "widths=128,128",
+                 "N=%d" % n_env, "T=%d" % T, "iters=%d" % iters, "seed=1"],
+                capture_output=True, text=True, timeout=600, check=True)
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            return {"value": round(r["env_steps_per_s"], 3),
+                    "unit": "env-steps/s", "cores": 1, "kind": "reference",
+                    "sample": sample}
+        except Exception as e:  # fall through to the port
+            print("cpu_baseline: reference harness failed: %s" % e,
+                  file=sys.stderr)
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd.trainer import init_policy, init_value
+    n_env, iters = 8, 3
+    pol = po.perbin_model(F0, [H1, H2], po.OR_SOFTMAX)
+    val = po.full_model(B * F0, [V1, V2], 1)
+    tr = po.Trainer(po.OR_PPO, B, D, n_env, T, pol, init_policy(D, H1, H2),
+                    val, init_value(B, D), x0=1)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        tr.rollout()
+        tr.learn()
+    dt = time.perf_counter() - t0
+    return {"value": round(n_env * T * iters / dt, 3), "unit": "env-steps/s",
+            "cores": 1, "kind": "port",
+            "sample": "oracle port, %d envs x T=%d x %d iterations" % (
+                n_env, T, iters)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    uid = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        from dependence_free_rl_amd import Context
+        obj = [Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+
+    from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
+                                        init_policy, init_value)
+    ctx = Context(device=local, rank=rank, world=world, uid=uid)
+    n = args.envs
+    tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=n, steps=T,
+                 widths=(H1, H2), value_widths=(V1, V2), rng_state=20241008,
+                 num_envs_global=n * world, env_offset=n * rank)
+    # random-init weights of the reference architecture (same on every rank)
+    tr.set_params(POLICY, init_policy(D, H1, H2, seed=0))
+    tr.set_params(VALUE, init_value(B, D, V1, V2, seed=1))
+
+    if args.warmup:
+        tr.iterate(args.warmup)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    tr.set_timing(True)
+    tr.reset_timing()
+    t0 = time.perf_counter()
+    tr.iterate(args.steps)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    ms_pt, n_pt = tr.kernel_time("policy_train")
+    ms_ro, n_ro = tr.kernel_time("rollout_step")
+    ms_v, _ = tr.kernel_time("value")
+    ms_r, _ = tr.kernel_time("reduce_sgd")
+    ms_a, _ = tr.kernel_time("allreduce")
+    env_steps = n * world * T * args.steps
+    value = env_steps / dt
+    # dominant kernel: policy_train (one PPO epoch over N*T env-steps);
+    # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
+    flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
+    avg_ms = ms_pt / max(n_pt, 1)
+    achieved = flops_epoch / (avg_ms * 1e-3) / 1e12
+    line = {
+        "metric": "env-steps/sec (whole node) PPO bin-packing 64-bin",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (fixed-size bin-packing instances, random-init "
+                "weights of the reference architecture)",
+        "config": {"workload": "BASELINE config %d: PPO, 2-D bin packing 64 "
+                               "bins, %d envs/GPU, per-bin policy [128,128], "
+                               "value [256,64,32], T=4, k=4"
+                               % (3 if world == 1 else 4, n),
+                   "envs_per_gpu": n, "bins": B, "dims": D, "T": T,
+                   "epochs": 4, "parallelism": "dp%d" % world},
+        "roofline": {"kernel": "policy_train", "bound": "mfma",
+                     "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "traffic": None,
+                     "avg_launch_ms": round(avg_ms, 4),
+                     "flops_per_launch": flops_epoch},
+        "phase_ms_per_step": {
+            "rollout": round(ms_ro / args.steps, 3),
+            "policy_train": round(ms_pt / args.steps, 3),
+            "value": round(ms_v / args.steps, 3),
+            "reduce_sgd": round(ms_r / args.steps, 3),
+            "allreduce": round(ms_a / args.steps, 3)},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    tr.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

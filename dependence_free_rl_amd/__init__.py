@@ -1,0 +1,9 @@
+"""dependence_free_rl_amd -- MI355X-native PPO / actor-critic rollout-and-update
+path for vectorised bin packing (drop-in for beehover/dependence_free_rl's
+xylo::rl / xylo::policy_gradient hot path).  See DESIGN.md."""
+from ._lib import XhError, lib  # noqa: F401  (fails loudly if not built)
+from .trainer import (ALGOS, POLICY, VALUE, Context, Trainer, init_policy,  # noqa: F401
+                      init_value, policy_param_count, value_param_count)
+
+__all__ = ["Context", "Trainer", "POLICY", "VALUE", "init_policy", "init_value",
+           "XhError"]

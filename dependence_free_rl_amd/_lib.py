@@ -1,0 +1,94 @@
+"""ctypes binding of the C ABI in include/xylo_hip.h (libxylo_hip.so).
+
+The library is the product: there is no CPU fallback.  If the in-tree
+``libxylo_hip.so`` is missing, importing this module raises immediately.
+"""
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libxylo_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "xylo_hip.h")
+
+XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)
+XH_PPO, XH_AC = 0, 1
+XH_POLICY, XH_VALUE = 0, 1
+(BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
+ BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
+ BUF_LOGITS, BUF_PROBS, BUF_V_STATE0) = range(15)
+
+
+class XhError(RuntimeError):
+    """A non-zero status from the C ABI (message from xh_last_error())."""
+
+
+class Config(C.Structure):
+    """Mirror of xh_config."""
+    _fields_ = [
+        ("algo", C.c_int), ("num_envs", C.c_int), ("num_envs_global", C.c_int),
+        ("env_offset", C.c_int), ("bins", C.c_int), ("dims", C.c_int),
+        ("steps", C.c_int), ("epochs", C.c_int), ("policy_h1", C.c_int),
+        ("policy_h2", C.c_int), ("value_h1", C.c_int), ("value_h2", C.c_int),
+        ("lr_policy", C.c_float), ("lr_value", C.c_float),
+        ("wd_policy", C.c_float), ("wd_value", C.c_float), ("gamma", C.c_float),
+        ("lambda_", C.c_float), ("clip_eps", C.c_float),
+        ("rng_state", C.c_uint32)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libxylo_hip.so not built (%s); run `make lib` or "
+            "__graft_entry__.build() -- there is no CPU fallback" % LIB_PATH)
+    lib = C.CDLL(LIB_PATH)
+    vp, i, sz = C.c_void_p, C.c_int, C.c_size_t
+    sig = {
+        "xh_last_error": (C.c_char_p, []),
+        "xh_version": (C.c_char_p, []),
+        "xh_comm_unique_id": (i, [vp]),
+        "xh_ctx_create": (i, [i, i, i, vp, C.POINTER(vp)]),
+        "xh_ctx_destroy": (i, [vp]),
+        "xh_ctx_synchronize": (i, [vp]),
+        "xh_ctx_allreduce_host": (i, [vp, vp, sz]),
+        "xh_config_default": (None, [C.POINTER(Config), i, i, i, i, i]),
+        "xh_trainer_create": (i, [vp, C.POINTER(Config), C.POINTER(vp)]),
+        "xh_trainer_destroy": (i, [vp]),
+        "xh_trainer_num_params": (sz, [vp, i]),
+        "xh_trainer_set_params": (i, [vp, i, vp, sz]),
+        "xh_trainer_get_params": (i, [vp, i, vp, sz]),
+        "xh_trainer_rollout": (i, [vp]),
+        "xh_trainer_learn": (i, [vp]),
+        "xh_trainer_iterate": (i, [vp, i]),
+        "xh_trainer_set_forced_actions": (i, [vp, vp]),
+        "xh_trainer_buffer_bytes": (sz, [vp, i]),
+        "xh_trainer_get_buffer": (i, [vp, i, vp, sz]),
+        "xh_trainer_set_buffer": (i, [vp, i, vp, sz]),
+        "xh_trainer_set_timing": (i, [vp, i]),
+        "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
+                                       C.POINTER(C.c_long)]),
+        "xh_trainer_reset_timing": (i, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status):
+    if status != XH_OK:
+        raise XhError("xylo-hip status %d: %s" % (
+            status, lib.xh_last_error().decode(errors="replace")))
+    return status
+
+
+def header_symbols():
+    """Function names declared by include/xylo_hip.h (for the ABI test)."""
+    with open(HEADER) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(xh_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,643 @@
+// policy_kernels.hip -- the per-bin policy on CDNA4 (gfx950):
+//
+//  * rollout_step_kernel: ONE kernel per environment step for all envs:
+//      obs encode (from int8 state) -> conv1d_1 F0->H1 -> relu -> H1->H2 ->
+//      relu -> H2->1 (MFMA f32 32x32x2) -> candidate-bin scores staged in LDS
+//      -> softmax (no max shift, nn.h:382-392) -> categorical sample
+//      (std::discrete_distribution over minstd_rand0, bit-exact) -> env apply /
+//      reward / reset (bin_packing.h:53-106) -> trajectory record.
+//  * policy_train_kernel: one PPO (or actor-critic) epoch over the batch:
+//      forward, clipped-surrogate (rl.h:54-74) or softmax-log (rl.h:45-52)
+//      loss gradient, softmax Jacobian backward (nn.h:393-417), Dense backward
+//      (nn.h:149-186) with dW accumulated on chip; one gradient slab per
+//      workgroup (reduced in slab order by reduce_sgd.hip: deterministic).
+//
+// Tiling (both kernels): a "group" is 64 rows = 64/B envs x B bins. Rows live
+// on MFMA lanes (col index), features in accumulator registers, so the
+// layer-1 accumulator feeds layer 2 as the B operand with no data movement
+// (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand").
+// W2 is staged once per workgroup in LDS (row stride H1+4: conflict-free
+// ds_read_b128 A-operand reads).  Weight gradients contract over rows, so
+// H1 and dL/dA2 go through LDS images (row stride +1) once per group.
+#include "xh_device.h"
+#include "xh_kernels.h"
+
+namespace xh {
+
+template <int B_, int D_, int H1_, int H2_>
+struct PShape {
+  static constexpr int B = B_, D = D_, H1 = H1_, H2 = H2_;
+  static constexpr int F0 = 2 * D;
+  static constexpr int S1 = (F0 + 1) / 2;  // layer-1 MFMA k-steps
+  static constexpr int NIT = H1 / 32, NOT = H2 / 32;
+  static constexpr int G = 64 / B;  // envs per 64-row group
+  static constexpr int BD = B * D;
+  static constexpr int W2S = H1 + 4;           // LDS W2 image row stride
+  static constexpr int HS = H1 + 1;            // LDS H1 image row stride
+  static constexpr int AS = H2 + 1;            // LDS dA2 image row stride
+  static constexpr int FJ = NOT >= 4 ? 2 : 1;  // fwd r-tiles per wave
+  static constexpr int JW = (NOT * NIT + 3) / 4;  // dW2 tiles per wave
+  static constexpr int JH = (2 * NIT + 3) / 4;    // dH1 r-tiles per wave
+  static_assert(B == 8 || B == 16 || B == 32 || B == 64, "B");
+  static_assert(NIT == 1 || NIT == 2 || NIT == 4, "H1 in {32,64,128}");
+  static_assert(NOT == 1 || NOT == 2 || NOT == 4, "H2 in {32,64,128}");
+  static_assert(D >= 1 && D <= 3, "D");
+  // LDS carve (floats), every region 16-byte aligned.
+  static constexpr int r4(int x) { return (x + 3) & ~3; }
+  static constexpr int L_W2 = 0;
+  static constexpr int L_W1 = L_W2 + H2 * W2S;
+  static constexpr int L_B1 = L_W1 + r4(H1 * F0);
+  static constexpr int L_B2 = L_B1 + H1;
+  static constexpr int L_W3 = L_B2 + H2;
+  static constexpr int L_B3 = L_W3 + H2;
+  static constexpr int L_Z = L_B3 + 4;
+  static constexpr int L_ROLLOUT_END = L_Z + NOT * 64;
+  static constexpr int L_H1 = L_ROLLOUT_END;
+  static constexpr int L_DA2 = L_H1 + r4(64 * HS);
+  static constexpr int L_TRAIN_END = L_DA2 + r4(64 * AS);
+  // end-of-kernel reduction scratch (aliases the H1 / dA2 images)
+  static constexpr int RED = H1 * F0 + H1 + 2 * H2 + 1;
+  static_assert(4 * RED <= 64 * HS + 64 * AS, "scratch fits");
+};
+
+// Stage the small per-bin parameters (all of layer 1/3, biases) and the W2
+// image into LDS.
+template <class S>
+__device__ __forceinline__ void stage_params(const float *__restrict__ P,
+                                             float *lds) {
+  const PolicyLayout L{S::F0, S::H1, S::H2};
+  const int tid = threadIdx.x;
+  for (int i = tid; i < S::H2 * S::H1; i += blockDim.x) {
+    const int o = i / S::H1, k = i - o * S::H1;
+    lds[S::L_W2 + o * S::W2S + k] = P[L.oW2() + i];
+  }
+  for (int i = tid; i < S::H1 * S::F0; i += blockDim.x)
+    lds[S::L_W1 + i] = P[L.oW1() + i];
+  for (int i = tid; i < S::H1; i += blockDim.x) lds[S::L_B1 + i] = P[L.ob1() + i];
+  for (int i = tid; i < S::H2; i += blockDim.x) {
+    lds[S::L_B2 + i] = P[L.ob2() + i];
+    lds[S::L_W3 + i] = P[L.ow3() + i];
+  }
+  if (tid == 0) lds[S::L_B3] = P[L.ob3()];
+}
+
+// Observation feature f of bin `bin` in env `env` at trajectory slot `slot`
+// (observation::to_vector, bin_packing.h:31-40): [bin dims / 8, item dims / 8].
+template <class S>
+__device__ __forceinline__ void load_row(const Batch &b, int slot, int env,
+                                         int bin, int (&bv)[S::D],
+                                         int (&iv)[S::D]) {
+  const int8_t *bp = b.bins + ((size_t)slot * b.N + env) * S::BD + bin * S::D;
+  const int8_t *ip = b.items + ((size_t)slot * b.N + env) * 4;
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) {
+    bv[d] = bp[d];
+    iv[d] = ip[d];
+  }
+}
+
+template <class S>
+__device__ __forceinline__ float feature(const int (&bv)[S::D],
+                                         const int (&iv)[S::D], int f) {
+  int v = 0;
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) {
+    if (f == d) v = bv[d];
+    if (f == S::D + d) v = iv[d];
+  }
+  return f < S::F0 ? (float)v / (float)kCapacity : 0.0f;
+}
+
+// Layer 1 (F0 -> H1) + bias + relu for the 64 rows of a group, all H1 tiles.
+// h1[it][rt]: col = row rt*32 + (lane&31), acc row = feature it*32+acc_row.
+template <class S>
+__device__ __forceinline__ void layer1(const Batch &b, int slot, int e0,
+                                       const float *lds,
+                                       f32x16 (&h1)[S::NIT][2]) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
+  float xb[2][S::S1];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int r = rt * 32 + lr;
+    int bv[S::D], iv[S::D];
+    load_row<S>(b, slot, e0 + r / S::B, r % S::B, bv, iv);
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) xb[rt][s] = feature<S>(bv, iv, 2 * s + h);
+  }
+#pragma unroll
+  for (int it = 0; it < S::NIT; ++it) {
+    float wa[S::S1];
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) {
+      const int k = 2 * s + h;
+      wa[s] = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int s = 0; s < S::S1; ++s) acc = mfma32(wa[s], xb[rt][s], acc);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float v = acc[j] + lds[S::L_B1 + it * 32 + acc_row(j, h)];
+        acc[j] = v > 0.0f ? v : 0.0f;
+      }
+      h1[it][rt] = acc;
+    }
+  }
+}
+
+// Layer 2 pre-activation (+ bias) for output tile o2t and r-tile rt:
+// A = W2 rows from the LDS image (4 k-steps per ds_read_b128), B = h1 regs.
+template <class S>
+__device__ __forceinline__ f32x16 layer2(const float *lds,
+                                         const f32x16 (&h1)[S::NIT][2],
+                                         int o2t, int rt) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
+  const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int it = 0; it < S::NIT; ++it) {
+    // select with a compile-time index (a runtime index would spill h1)
+    const f32x16 hb = rt == 0 ? h1[it][0] : h1[it][1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a4 = *reinterpret_cast<const float4 *>(wrow + it * 32 + 8 * q);
+      acc = mfma32(a4.x, hb[4 * q + 0], acc);
+      acc = mfma32(a4.y, hb[4 * q + 1], acc);
+      acc = mfma32(a4.z, hb[4 * q + 2], acc);
+      acc = mfma32(a4.w, hb[4 * q + 3], acc);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] += lds[S::L_B2 + o2t * 32 + acc_row(j, h)];
+  return acc;
+}
+
+// Partial logit over this tile's 32 H2 units for row rt*32 + (lane&31).
+template <class S>
+__device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
+                                            int o2t) {
+  const int h = (threadIdx.x & 63) >> 5;
+  float zp = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float v = pre[j] > 0.0f ? pre[j] : 0.0f;
+    zp += v * lds[S::L_W3 + o2t * 32 + acc_row(j, h)];
+  }
+  return zp + __shfl_xor(zp, 32, kWave);
+}
+
+// =========================================================== rollout step ==
+template <class S>
+__global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31;
+  const int N = a.b.N, t = a.t;
+  const int ngroups = N / S::G;
+  // forward job of this wave: output tile o2t, r-tiles rt0 .. rt0+FJ-1
+  const int o2t = w % S::NOT;
+  const int rt0 = S::NOT >= 4 ? 0 : w / S::NOT;
+  const bool fwd_active = (w / S::NOT) * S::FJ < 2;
+
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int e0 = g * S::G;
+    {
+      f32x16 h1[S::NIT][2];
+      layer1<S>(a.b, t, e0, lds, h1);
+      if (fwd_active) {
+#pragma unroll
+        for (int q = 0; q < S::FJ; ++q) {
+          const int rt = rt0 + q;
+          const f32x16 pre = layer2<S>(lds, h1, o2t, rt);
+          const float zp = logit_part<S>(lds, pre, o2t);
+          if (lane < 32) lds[S::L_Z + o2t * 64 + rt * 32 + lr] = zp;
+        }
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      // ---- candidate-bin scores -> softmax -> sample -> env step (lane=row)
+      constexpr int B = S::B;
+      const int e = lane / B, bin = lane % B, env = e0 + e, seg0 = e * B;
+      float zs = 0.0f;
+#pragma unroll
+      for (int o = 0; o < S::NOT; ++o) zs += lds[S::L_Z + o * 64 + lane];
+      const float z = zs + lds[S::L_B3];
+      const float ex = expf(z);
+      const float sum = seg_sum<B>(ex);
+      const float p = ex / sum;
+      if (a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
+      if (a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
+
+      uint32_t x = a.b.rng[env];
+      int choice;
+      if (a.forced) {
+        choice = a.forced[(size_t)t * N + env];
+        (void)canonical(x);  // the sampler's two engine draws
+      } else {
+        // std::discrete_distribution (random.tcc:2654-2713): p -> double,
+        // normalise by the sum, partial sums, last = 1, lower_bound(u).
+        const double pd = (double)p;
+        const double sd = seg_sum_d<B>(pd);
+        double cp = seg_scan_d<B>(pd / sd, lane);
+        if (bin == B - 1) cp = 1.0;
+        const double u = canonical(x);
+        const unsigned long long below = __ballot(cp < u);
+        unsigned long long segmask = ~0ull;
+        if constexpr (B < 64) segmask = ((1ull << B) - 1ull) << seg0;
+        choice = __popcll(below & segmask);
+        // Near a cumulative boundary the tree-ordered sums could round
+        // differently from the sequential ones: recompute sequentially.
+        const float gap = (float)fabs(cp - u);
+        if (seg_min<B>(gap) < 1e-9f) {
+          double s2 = 0.0;
+          for (int k = 0; k < B; ++k) s2 += (double)wave_shfl(p, seg0 + k);
+          double acc = 0.0;
+          int c2 = B - 1;
+          for (int k = 0; k < B; ++k) {
+            const double qk = (double)wave_shfl(p, seg0 + k) / s2;
+            acc = k == 0 ? qk : acc + qk;
+            const double cpk = k == B - 1 ? 1.0 : acc;
+            if (!(cpk < u) && k < c2) c2 = k;
+          }
+          choice = c2;
+        }
+      }
+      const float pold = wave_shfl(p, seg0 + choice);
+
+      int bv[S::D], iv[S::D];
+      load_row<S>(a.b, t, env, bin, bv, iv);
+      int nb[S::D];
+      int neg = 0;
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) {
+        nb[d] = bin == choice ? bv[d] - iv[d] : bv[d];
+        neg |= nb[d] < 0;
+      }
+      const int done = __shfl(neg, seg0 + choice, kWave);
+      // apply -> get_item, or game over -> reset -> get_item: 2 draws either way
+      const bool first = canonical(x) < a.env.p_a;
+      int8_t *ob = a.b.bins + ((size_t)(t + 1) * N + env) * S::BD + bin * S::D;
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) ob[d] = (int8_t)(done ? kCapacity : nb[d]);
+      if (bin == 0) {
+        int8_t *oi = a.b.items + ((size_t)(t + 1) * N + env) * 4;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+        a.b.action[(size_t)t * N + env] = choice;
+        a.b.pold[(size_t)t * N + env] = pold;
+        a.b.done[(size_t)t * N + env] = (uint8_t)done;
+        a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================ train epoch ==
+template <class S>
+__global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  constexpr int B = S::B, NIT = S::NIT, NOT = S::NOT;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int N = a.b.N, T = a.b.T;
+  const int gpt = N / S::G;  // groups per step
+  const int ngroups = T * gpt;
+  float *H1img = lds + S::L_H1;
+  float *DAimg = lds + S::L_DA2;
+
+  // wave roles (see header comment)
+  const int o2t = w % NOT;
+  const int rt0 = NOT >= 4 ? 0 : w / NOT;
+  const bool fwd_active = (w / NOT) * S::FJ < 2;
+  const int it_own = w % NIT;             // dH1 / dW1 tile
+  const int hrt0 = w / NIT;               // first dH1 r-tile
+  constexpr int HSTEP = 4 / NIT;          // r-tile stride between slots
+
+  // persistent accumulators
+  f32x16 accW2[S::JW];
+#pragma unroll
+  for (int q = 0; q < S::JW; ++q) accW2[q] = zero16();
+  float accW1[16][S::F0], accB1[16], accW3[16], accB2[16], accB3 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    accB1[j] = accW3[j] = accB2[j] = 0.0f;
+#pragma unroll
+    for (int f = 0; f < S::F0; ++f) accW1[j][f] = 0.0f;
+  }
+
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int t = g / gpt, e0 = (g - t * gpt) * S::G;
+    f32x16 pre[S::FJ];
+    f32x16 h1own[2];
+    {
+      f32x16 h1[NIT][2];
+      layer1<S>(a.b, t, e0, lds, h1);
+      // H1 image for dW2 (each H1 tile written by one wave)
+      if (w < NIT) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it)
+          if (it == w) {
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+              for (int j = 0; j < 16; ++j)
+                H1img[(rt * 32 + lr) * S::HS + it * 32 + acc_row(j, h)] =
+                    h1[it][rt][j];
+          }
+      }
+#pragma unroll
+      for (int it = 0; it < NIT; ++it)
+        if (it == it_own) {
+          h1own[0] = h1[it][0];
+          h1own[1] = h1[it][1];
+        }
+      if (fwd_active) {
+#pragma unroll
+        for (int q = 0; q < S::FJ; ++q) {
+          const int rt = rt0 + q;
+          pre[q] = layer2<S>(lds, h1, o2t, rt);
+          const float zp = logit_part<S>(lds, pre[q], o2t);
+          if (lane < 32) lds[S::L_Z + o2t * 64 + rt * 32 + lr] = zp;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- logits -> softmax -> loss gradient w.r.t. logits (lane = row)
+    float gz;
+    {
+      const int e = lane / B, bin = lane % B, env = e0 + e, seg0 = e * B;
+      float zs = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NOT; ++o) zs += lds[S::L_Z + o * 64 + lane];
+      const float z = zs + lds[S::L_B3];
+      const float ex = expf(z);
+      const float p = ex / seg_sum<B>(ex);
+      const size_t ti = (size_t)t * N + env;
+      const int c = a.b.action[ti];
+      const float A = a.adv[ti];
+      if (a.algo == kPPO) {
+        // clipped_gradient (rl.h:54-74) then softmax_layer::backward
+        // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
+        const float pc = wave_shfl(p, seg0 + c);
+        const float ratio = pc / a.b.pold[ti];
+        float clipped = ratio;
+        if (ratio > 1.0f + a.clip_eps)
+          clipped = 1.0f + a.clip_eps;
+        else if (ratio < 1.0f - a.clip_eps)
+          clipped = 1.0f - a.clip_eps;
+        const float ig = fminf(clipped * A, ratio * A) * -1.0f;
+        const float gc = ig / pc;
+        const float lin = bin == c ? p : 0.0f;
+        gz = (lin - p * pc) * gc;
+      } else {
+        // softmax_gradient_log (rl.h:45-52) through softmax-xent (identity)
+        gz = p * A;
+        if (bin == c) gz -= A;
+      }
+      if (w == 0) accB3 += gz;
+    }
+
+    // ---- backward through layer 3 and the layer-2 relu (fwd tiles)
+    if (fwd_active) {
+#pragma unroll
+      for (int q = 0; q < S::FJ; ++q) {
+        const int rt = rt0 + q;
+        const float gr = wave_shfl(gz, rt * 32 + lr);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int o2 = o2t * 32 + acc_row(j, h);
+          const float v = pre[q][j];
+          const float h2 = v > 0.0f ? v : 0.0f;
+          accW3[j] += gr * h2;
+          const float d = v > 0.0f ? gr * lds[S::L_W3 + o2] : 0.0f;
+          accB2[j] += d;
+          DAimg[(rt * 32 + lr) * S::AS + o2] = d;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows)
+#pragma unroll
+    for (int q = 0; q < S::JW; ++q) {
+      const int it = w / NOT + q * (4 / NOT);
+      if (it < NIT) {
+        f32x16 acc = accW2[q];
+#pragma unroll 8
+        for (int s = 0; s < 32; ++s) {
+          const int r = 2 * s + h;
+          acc = mfma32(DAimg[r * S::AS + o2t * 32 + lr],
+                       H1img[r * S::HS + it * 32 + lr], acc);
+        }
+        accW2[q] = acc;
+      }
+    }
+
+    // ---- dH1^T[i][r] = sum_o2 W2[o2][i] dA2[r][o2]; relu'; dW1, db1
+#pragma unroll
+    for (int q = 0; q < S::JH; ++q) {
+      const int rt = hrt0 + q * HSTEP;
+      if (rt < 2) {
+        f32x16 acc = zero16();
+#pragma unroll 8
+        for (int s = 0; s < S::H2 / 2; ++s) {
+          const int k = 2 * s + h;
+          acc = mfma32(lds[S::L_W2 + k * S::W2S + it_own * 32 + lr],
+                       DAimg[(rt * 32 + lr) * S::AS + k], acc);
+        }
+        const int r = rt * 32 + lr;
+        int bv[S::D], iv[S::D];
+        load_row<S>(a.b, t, e0 + r / B, r % B, bv, iv);
+        float xf[S::F0];
+#pragma unroll
+        for (int f = 0; f < S::F0; ++f) xf[f] = feature<S>(bv, iv, f);
+        const f32x16 hv = (rt == 0) ? h1own[0] : h1own[1];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float d = hv[j] > 0.0f ? acc[j] : 0.0f;
+          accB1[j] += d;
+#pragma unroll
+          for (int f = 0; f < S::F0; ++f) accW1[j][f] += d * xf[f];
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------- slab write-out ----
+  const PolicyLayout L{S::F0, S::H1, S::H2};
+  float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int q = 0; q < S::JW; ++q) {
+    const int it = w / NOT + q * (4 / NOT);
+    if (it < NIT) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int o2 = o2t * 32 + acc_row(j, h);
+        slab[L.oW2() + o2 * S::H1 + it * 32 + lr] = accW2[q][j];
+      }
+    }
+  }
+  // per-lane partials -> sum over the 32 lanes of each half -> LDS scratch
+  // [wave][RED] -> ordered sum over waves.
+  float *scr = lds + S::L_H1;
+  for (int i = threadIdx.x; i < 4 * S::RED; i += blockDim.x) scr[i] = 0.0f;
+  __syncthreads();
+  float *my = scr + w * S::RED;
+  // layout inside RED: [dW1 (H1*F0)] [db1 (H1)] [dw3 (H2)] [db2 (H2)] [db3]
+  const bool h_active = hrt0 < 2;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    float vb1 = accB1[j], vw3 = accW3[j], vb2 = accB2[j];
+    float vw1[S::F0];
+#pragma unroll
+    for (int f = 0; f < S::F0; ++f) vw1[f] = accW1[j][f];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      vb1 += __shfl_xor(vb1, o, kWave);
+      vw3 += __shfl_xor(vw3, o, kWave);
+      vb2 += __shfl_xor(vb2, o, kWave);
+#pragma unroll
+      for (int f = 0; f < S::F0; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
+    }
+    if (lr == 0) {
+      const int i = it_own * 32 + acc_row(j, h);
+      const int o2 = o2t * 32 + acc_row(j, h);
+      if (h_active) {
+#pragma unroll
+        for (int f = 0; f < S::F0; ++f) my[i * S::F0 + f] = vw1[f];
+        my[S::H1 * S::F0 + i] = vb1;
+      }
+      if (fwd_active) {
+        my[S::H1 * S::F0 + S::H1 + o2] = vw3;
+        my[S::H1 * S::F0 + S::H1 + S::H2 + o2] = vb2;
+      }
+    }
+  }
+  {
+    float v = accB3;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+    if (w == 0 && lane == 0) my[S::RED - 1] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < S::RED; i += blockDim.x) {
+    const float v = ((scr[i] + scr[S::RED + i]) + scr[2 * S::RED + i]) +
+                    scr[3 * S::RED + i];
+    int dst;
+    if (i < S::H1 * S::F0)
+      dst = L.oW1() + i;
+    else if (i < S::H1 * S::F0 + S::H1)
+      dst = L.ob1() + (i - S::H1 * S::F0);
+    else if (i < S::H1 * S::F0 + S::H1 + S::H2)
+      dst = L.ow3() + (i - S::H1 * S::F0 - S::H1);
+    else if (i < S::RED - 1)
+      dst = L.ob2() + (i - S::H1 * S::F0 - S::H1 - S::H2);
+    else
+      dst = L.ob3();
+    slab[dst] = v;
+  }
+}
+
+// ================================================================ dispatch ==
+#define XH_POLICY_SHAPES(X) \
+  X(8, 2, 128, 64)          \
+  X(8, 2, 64, 32)           \
+  X(16, 2, 64, 64)          \
+  X(32, 1, 64, 64)          \
+  X(64, 2, 128, 128)
+
+template <class S>
+constexpr size_t rollout_lds() {
+  return sizeof(float) * S::L_ROLLOUT_END;
+}
+template <class S>
+constexpr size_t train_lds() {
+  return sizeof(float) * S::L_TRAIN_END;
+}
+
+bool policy_shape_supported(int B, int D, int H1, int H2) {
+#define X(XB, XD, XH1, XH2) \
+  if (B == XB && D == XD && H1 == XH1 && H2 == XH2) return true;
+  XH_POLICY_SHAPES(X)
+#undef X
+  return false;
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+            hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+int rollout_grid(int B, int D, int H1, int H2) {
+  (void)B; (void)D; (void)H1; (void)H2;
+  return 2 * cu_count();
+}
+int policy_train_grid(int B, int D, int H1, int H2) {
+  (void)B; (void)D; (void)H1; (void)H2;
+  return cu_count();
+}
+
+hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
+                               hipStream_t s) {
+  const int B = a.env.B, D = a.env.D;
+#define X(XB, XD, XH1, XH2)                                                  \
+  if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
+    using S = PShape<XB, XD, XH1, XH2>;                                      \
+    static bool attr = false;                                                \
+    if (!attr) {                                                             \
+      (void)hipFuncSetAttribute((const void *)rollout_step_kernel<S>,        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                (int)rollout_lds<S>());                      \
+      attr = true;                                                           \
+    }                                                                        \
+    const int ng = a.b.N / S::G;                                             \
+    hipLaunchKernelGGL(rollout_step_kernel<S>, dim3(grid < ng ? grid : ng),  \
+                       dim3(256), rollout_lds<S>(), s, a);                   \
+    return hipGetLastError();                                                \
+  }
+  XH_POLICY_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
+                               int grid, hipStream_t s) {
+  const int B = a.env.B, D = a.env.D;
+#define X(XB, XD, XH1, XH2)                                                  \
+  if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
+    using S = PShape<XB, XD, XH1, XH2>;                                      \
+    static bool attr = false;                                                \
+    if (!attr) {                                                             \
+      (void)hipFuncSetAttribute((const void *)policy_train_kernel<S>,        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                (int)train_lds<S>());                        \
+      attr = true;                                                           \
+    }                                                                        \
+    hipLaunchKernelGGL(policy_train_kernel<S>, dim3(grid), dim3(256),        \
+                       train_lds<S>(), s, a);                                \
+    return hipGetLastError();                                                \
+  }
+  XH_POLICY_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace xh

@@ -1,0 +1,128 @@
+// xh_kernels.h -- kernel argument blocks and launch entry points shared by the
+// host runtime (xylo_hip.cpp) and the HIP kernel files.  No torch types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xh {
+
+enum Algo { kPPO = 0, kAC = 1 };
+
+// Flat parameter offsets of the per-bin policy, in the reference layout
+// model::parameters() (nn.h:499-508): conv1d_1(F0->H1), relu,
+// conv1d_1(H1->H2), relu, conv1d_1(H2->1), head.  Each dense layer stores
+// [A(out x in) row-major, b(out)].
+struct PolicyLayout {
+  int F0, H1, H2;
+  __host__ __device__ int oW1() const { return 0; }
+  __host__ __device__ int ob1() const { return H1 * F0; }
+  __host__ __device__ int oW2() const { return ob1() + H1; }
+  __host__ __device__ int ob2() const { return oW2() + H2 * H1; }
+  __host__ __device__ int ow3() const { return ob2() + H2; }
+  __host__ __device__ int ob3() const { return ow3() + H2; }
+  __host__ __device__ int size() const { return ob3() + 1; }
+};
+
+// Value net: full(Fin->V1), relu, full(V1->V2), relu, full(V2->1)
+// (ppo_training.cc:19-26).
+struct ValueLayout {
+  int Fin, V1, V2;
+  __host__ __device__ int oW1() const { return 0; }
+  __host__ __device__ int ob1() const { return V1 * Fin; }
+  __host__ __device__ int oW2() const { return ob1() + V1; }
+  __host__ __device__ int ob2() const { return oW2() + V2 * V1; }
+  __host__ __device__ int ow3() const { return ob2() + V2; }
+  __host__ __device__ int ob3() const { return ow3() + V2; }
+  __host__ __device__ int size() const { return ob3() + 1; }
+};
+
+// Environment description (bin_packing.h:46-85, generalised to D dims).
+struct EnvDesc {
+  int B, D;
+  int item_a[3], item_b[3];
+  double p_a;
+};
+
+// Per-iteration trajectory storage (device).  Slot t of `bins`/`items` is the
+// state S_t before step t; slot T is the state after the last step (the next
+// iteration's S_0).  Terminal states E_t are recomputed from S_t + action.
+struct Batch {
+  int N, T;
+  int8_t *bins;     // [T+1][N][B*D]
+  int8_t *items;    // [T+1][N][4]
+  int32_t *action;  // [T][N]
+  float *pold;      // [T][N]   distrib[choice] at sampling time (rl.h:29)
+  uint8_t *done;    // [T][N]
+  uint32_t *rng;    // [N]      per-env minstd_rand0 state (reference order)
+};
+
+struct RolloutArgs {
+  EnvDesc env;
+  Batch b;
+  int t;              // step index within the iteration
+  uint32_t jump_mul;  // a^(4T(Nglobal-1)) mod m, applied after step T-1
+  const float *params;
+  const int32_t *forced;  // optional [T][N] actions (teacher forcing)
+  float *logits_out;      // optional [N][B] (debug / parity)
+  float *probs_out;       // optional [N][B]
+};
+
+struct PolicyTrainArgs {
+  EnvDesc env;
+  Batch b;
+  int algo;
+  float clip_eps;
+  const float *params;
+  const float *adv;  // [T][N]
+  float *slab;       // [gridDim.x][slab_stride]
+  int slab_stride;
+};
+
+struct ValueArgs {
+  EnvDesc env;
+  Batch b;
+  const float *params;   // flat value params
+  const float *w1t;      // [Fin][V1] transposed copy of W1 (row per feature)
+  float *v_state;        // [T+1][N]   V(S_t)
+  float *v_term;         // [T][N]     V(E_t) (terminal view of step t)
+  int with_term;         // eval: also evaluate the terminal views
+  // value-step row buffers (train mode)
+  const float *targets;  // [T][N]
+  float *row_g;          // [T*N]       V - target
+  float *row_h1;         // [T*N][V1]   post-relu layer-1 activations
+  float *row_h2;         // [T*N][V2]
+  float *row_d1;         // [T*N][V1]   dL/d(pre-act layer 1)
+  float *row_d2;         // [T*N][V2]
+};
+
+// Launchers (return hipError_t of the launch). `variant` selects the
+// <B,D,H1,H2> instantiation; returns hipErrorInvalidValue when unsupported.
+bool policy_shape_supported(int B, int D, int H1, int H2);
+hipError_t launch_env_init(const EnvDesc &env, Batch b, uint32_t x0,
+                           int env_offset, int n_global, hipStream_t s);
+hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
+                               hipStream_t s);
+hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
+                               int grid, hipStream_t s);
+int policy_train_grid(int B, int D, int H1, int H2);
+int rollout_grid(int B, int D, int H1, int H2);
+
+bool value_shape_supported(int V1, int V2);
+hipError_t launch_value_eval(const ValueArgs &a, int V1, int V2,
+                             hipStream_t s);
+hipError_t launch_value_rows(const ValueArgs &a, int V1, int V2,
+                             hipStream_t s);
+hipError_t launch_value_wgrad(const ValueArgs &a, int V1, int V2, float *slab,
+                              int slab_stride, int grid, hipStream_t s);
+hipError_t launch_value_targets(const ValueArgs &a, float gamma, float *targets,
+                                hipStream_t s);
+hipError_t launch_gae(const ValueArgs &a, float gamma, float lambda, float *adv,
+                      hipStream_t s);
+hipError_t launch_transpose(const float *src, float *dst, int rows, int cols,
+                            hipStream_t s);
+hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
+                              float *out, hipStream_t s);
+hipError_t launch_sgd(float *params, const float *grad, int n, float lr,
+                      float wd, hipStream_t s);
+
+}  // namespace xh

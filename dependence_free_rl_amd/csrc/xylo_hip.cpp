@@ -1,0 +1,759 @@
+// xylo_hip.cpp -- host runtime behind the C ABI (include/xylo_hip.h).
+//
+// One xh_trainer owns every device buffer of the vectorised PPO / AC path and
+// drives it on one HIP stream: T rollout-step kernels, then learn() in the
+// reference order (policy_gradient.h:159-185): value eval -> TD targets ->
+// value SGD step -> value re-eval -> GAE -> k policy epochs.  With world > 1
+// each flat gradient is SUM-all-reduced with RCCL on the same stream before
+// the identical SGD step on every rank (the reference's loss is a sum over
+// rows, nn.h:94-98, so the sharded sum equals the single-process gradient).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/xylo_hip.h"
+#include "xh_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                         \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess)                                                 \
+      return fail(XH_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #x,     \
+                  hipGetErrorString(e_));                                 \
+  } while (0)
+
+#define RCCLCHK(x)                                                        \
+  do {                                                                    \
+    ncclResult_t r_ = (x);                                                \
+    if (r_ != ncclSuccess)                                                \
+      return fail(XH_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #x,    \
+                  ncclGetErrorString(r_));                                \
+  } while (0)
+
+#define CHK(x)                   \
+  do {                           \
+    int s_ = (x);                \
+    if (s_ != XH_OK) return s_;  \
+  } while (0)
+
+// No exception may cross the ABI.
+template <class F>
+int guard(F &&f) {
+  try {
+    return f();
+  } catch (const std::exception &e) {
+    return fail(XH_ERR_INVALID, "exception: %s", e.what());
+  } catch (...) {
+    return fail(XH_ERR_INVALID, "unknown exception");
+  }
+}
+
+uint32_t mstd_pow(uint64_t k) {  // 16807^k mod (2^31-1)
+  uint64_t acc = 1, base = 16807;
+  while (k) {
+    if (k & 1) acc = acc * base % 2147483647ull;
+    base = base * base % 2147483647ull;
+    k >>= 1;
+  }
+  return (uint32_t)acc;
+}
+
+}  // namespace
+
+struct xh_ctx {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+};
+
+struct timed_event {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+struct xh_trainer {
+  xh_ctx *ctx = nullptr;
+  xh_config cfg{};
+  xh::EnvDesc env{};
+  xh::PolicyLayout pl{};
+  xh::ValueLayout vl{};
+  int np = 0, nv = 0;
+  // trajectory batch
+  int8_t *bins = nullptr, *items = nullptr;
+  int32_t *action = nullptr, *forced = nullptr;
+  float *pold = nullptr;
+  uint8_t *done = nullptr;
+  uint32_t *rng = nullptr;
+  // parameters and learner buffers
+  float *pp = nullptr, *vp = nullptr, *vw1t = nullptr;
+  float *v_state = nullptr, *v_state0 = nullptr, *v_term = nullptr;
+  float *targets = nullptr, *adv = nullptr;
+  float *row_g = nullptr, *row_h1 = nullptr, *row_h2 = nullptr,
+        *row_d1 = nullptr, *row_d2 = nullptr;
+  float *pslab = nullptr, *vslab = nullptr;
+  int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
+  float *pgrads = nullptr, *vgrad = nullptr;
+  float *logits = nullptr, *probs = nullptr;
+  uint32_t jump_mul = 1;
+  int rgrid = 0;
+  bool need_shift = false;
+  bool use_forced = false;
+  bool timing = false;
+  std::vector<timed_event> events;
+  std::vector<void *> allocs;
+
+  xh::Batch batch() const {
+    xh::Batch b;
+    b.N = cfg.num_envs;
+    b.T = cfg.steps;
+    b.bins = bins;
+    b.items = items;
+    b.action = action;
+    b.pold = pold;
+    b.done = done;
+    b.rng = rng;
+    return b;
+  }
+  xh::ValueArgs vargs() const {
+    xh::ValueArgs a{};
+    a.env = env;
+    a.b = batch();
+    a.params = vp;
+    a.w1t = vw1t;
+    a.v_state = v_state;
+    a.v_term = v_term;
+    a.targets = targets;
+    a.row_g = row_g;
+    a.row_h1 = row_h1;
+    a.row_h2 = row_h2;
+    a.row_d1 = row_d1;
+    a.row_d2 = row_d2;
+    return a;
+  }
+  size_t N() const { return (size_t)cfg.num_envs; }
+  size_t T() const { return (size_t)cfg.steps; }
+  size_t BD() const { return (size_t)cfg.bins * cfg.dims; }
+};
+
+namespace {
+
+template <class P>
+int dalloc(xh_trainer *t, P **p, size_t bytes) {
+  void *q = nullptr;
+  HIPCHK(hipMalloc(&q, bytes < 16 ? 16 : bytes));
+  HIPCHK(hipMemset(q, 0, bytes < 16 ? 16 : bytes));
+  t->allocs.push_back(q);
+  *p = reinterpret_cast<P *>(q);
+  return XH_OK;
+}
+
+// Launch wrapper: optional HIP-event timing on the trainer's stream.
+template <class F>
+int timed(xh_trainer *t, const char *name, F &&launch) {
+  hipStream_t s = t->ctx->stream;
+  timed_event ev;
+  if (t->timing) {
+    ev.name = name;
+    HIPCHK(hipEventCreate(&ev.start));
+    HIPCHK(hipEventCreate(&ev.stop));
+    HIPCHK(hipEventRecord(ev.start, s));
+  }
+  hipError_t e = launch();
+  if (e != hipSuccess)
+    return fail(XH_ERR_HIP, "launch %s: %s", name, hipGetErrorString(e));
+  if (t->timing) {
+    HIPCHK(hipEventRecord(ev.stop, s));
+    t->events.push_back(ev);
+  }
+  return XH_OK;
+}
+
+int allreduce(xh_trainer *t, float *buf, int n) {
+  if (t->ctx->world <= 1) return XH_OK;
+  hipStream_t s = t->ctx->stream;
+  return timed(t, "allreduce", [&]() -> hipError_t {
+    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum,
+                                   t->ctx->comm, s);
+    return r == ncclSuccess ? hipSuccess : hipErrorUnknown;
+  });
+}
+
+size_t buffer_bytes(const xh_trainer *t, int which) {
+  const size_t N = t->N(), T = t->T();
+  switch (which) {
+    case XH_BUF_BINS: return (T + 1) * N * t->BD();
+    case XH_BUF_ITEMS: return (T + 1) * N * 4;
+    case XH_BUF_ACTION: return T * N * 4;
+    case XH_BUF_POLD: return T * N * 4;
+    case XH_BUF_DONE: return T * N;
+    case XH_BUF_RNG: return N * 4;
+    case XH_BUF_V_STATE: return (T + 1) * N * 4;
+    case XH_BUF_V_STATE0: return (T + 1) * N * 4;
+    case XH_BUF_V_TERM: return T * N * 4;
+    case XH_BUF_TARGETS: return T * N * 4;
+    case XH_BUF_ADV: return T * N * 4;
+    case XH_BUF_VALUE_GRAD: return (size_t)t->nv * 4;
+    case XH_BUF_POLICY_GRADS: return (size_t)t->cfg.epochs * t->np * 4;
+    case XH_BUF_LOGITS: return N * t->cfg.bins * 4;
+    case XH_BUF_PROBS: return N * t->cfg.bins * 4;
+  }
+  return 0;
+}
+
+void *buffer_ptr(const xh_trainer *t, int which) {
+  switch (which) {
+    case XH_BUF_BINS: return t->bins;
+    case XH_BUF_ITEMS: return t->items;
+    case XH_BUF_ACTION: return t->action;
+    case XH_BUF_POLD: return t->pold;
+    case XH_BUF_DONE: return t->done;
+    case XH_BUF_RNG: return t->rng;
+    case XH_BUF_V_STATE: return t->v_state;
+    case XH_BUF_V_STATE0: return t->v_state0;
+    case XH_BUF_V_TERM: return t->v_term;
+    case XH_BUF_TARGETS: return t->targets;
+    case XH_BUF_ADV: return t->adv;
+    case XH_BUF_VALUE_GRAD: return t->vgrad;
+    case XH_BUF_POLICY_GRADS: return t->pgrads;
+    case XH_BUF_LOGITS: return t->logits;
+    case XH_BUF_PROBS: return t->probs;
+  }
+  return nullptr;
+}
+
+int refresh_value_transpose(xh_trainer *t) {
+  return timed(t, "value", [&]() {
+    return xh::launch_transpose(t->vp + t->vl.oW1(), t->vw1t, t->vl.V1,
+                                t->vl.Fin, t->ctx->stream);
+  });
+}
+
+int do_rollout(xh_trainer *t) {
+  hipStream_t s = t->ctx->stream;
+  const size_t N = t->N(), T = t->T();
+  if (t->need_shift) {  // replay_buffer::forget(): open trajectories continue
+    HIPCHK(hipMemcpyAsync(t->bins, t->bins + T * N * t->BD(), N * t->BD(),
+                          hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(t->items, t->items + T * N * 4, N * 4,
+                          hipMemcpyDeviceToDevice, s));
+    t->need_shift = false;
+  }
+  xh::RolloutArgs a{};
+  a.env = t->env;
+  a.b = t->batch();
+  a.jump_mul = t->jump_mul;
+  a.params = t->pp;
+  a.forced = t->use_forced ? t->forced : nullptr;
+  for (int step = 0; step < (int)T; ++step) {
+    a.t = step;
+    const bool last = step == (int)T - 1;
+    a.logits_out = last ? t->logits : nullptr;
+    a.probs_out = last ? t->probs : nullptr;
+    CHK(timed(t, "rollout_step", [&]() {
+      return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
+                                     t->rgrid, s);
+    }));
+  }
+  return XH_OK;
+}
+
+int do_learn(xh_trainer *t) {
+  hipStream_t s = t->ctx->stream;
+  const xh_config &c = t->cfg;
+  xh::ValueArgs va = t->vargs();
+  // update_value_model (policy_gradient.h:196-218)
+  va.v_state = t->v_state0;
+  va.with_term = 1;
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_value_eval(va, c.value_h1, c.value_h2, s);
+  }));
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_value_targets(va, c.gamma, t->targets, s);
+  }));
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_value_rows(va, c.value_h1, c.value_h2, s);
+  }));
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_value_wgrad(va, c.value_h1, c.value_h2, t->vslab,
+                                  t->vslab_stride, t->vslab_n, s);
+  }));
+  CHK(timed(t, "reduce_sgd", [&]() {
+    return xh::launch_slab_reduce(t->vslab, t->vslab_n, t->vslab_stride, t->nv,
+                                  t->vgrad, s);
+  }));
+  CHK(allreduce(t, t->vgrad, t->nv));
+  CHK(timed(t, "reduce_sgd", [&]() {
+    return xh::launch_sgd(t->vp, t->vgrad, t->nv, c.lr_value, c.wd_value, s);
+  }));
+  CHK(refresh_value_transpose(t));
+  // calculate_advantage (policy_gradient.h:220-281): post-update values
+  va.v_state = t->v_state;
+  va.with_term = 0;  // GAE zeroes V(terminal); keep eval-1 V(E_t) for targets
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_value_eval(va, c.value_h1, c.value_h2, s);
+  }));
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_gae(va, c.gamma, c.lambda, t->adv, s);
+  }));
+  // optimize_action: k policy steps (policy_gradient.h:297-307)
+  xh::PolicyTrainArgs pa{};
+  pa.env = t->env;
+  pa.b = t->batch();
+  pa.algo = c.algo;
+  pa.clip_eps = c.clip_eps;
+  pa.params = t->pp;
+  pa.adv = t->adv;
+  pa.slab = t->pslab;
+  pa.slab_stride = t->pslab_stride;
+  for (int e = 0; e < c.epochs; ++e) {
+    float *g = t->pgrads + (size_t)e * t->np;
+    CHK(timed(t, "policy_train", [&]() {
+      return xh::launch_policy_train(pa, c.policy_h1, c.policy_h2, t->pslab_n,
+                                     s);
+    }));
+    CHK(timed(t, "reduce_sgd", [&]() {
+      return xh::launch_slab_reduce(t->pslab, t->pslab_n, t->pslab_stride,
+                                    t->np, g, s);
+    }));
+    CHK(allreduce(t, g, t->np));
+    CHK(timed(t, "reduce_sgd", [&]() {
+      return xh::launch_sgd(t->pp, g, t->np, c.lr_policy, c.wd_policy, s);
+    }));
+  }
+  t->need_shift = true;
+  return XH_OK;
+}
+
+}  // namespace
+
+// ================================================================= C ABI ==
+extern "C" {
+
+const char *xh_last_error(void) { return g_err.c_str(); }
+const char *xh_version(void) { return "xylo-hip 0.1 (gfx950)"; }
+
+int xh_comm_unique_id(void *out128) {
+  return guard([&]() -> int {
+    if (!out128) return fail(XH_ERR_INVALID, "null out");
+    ncclUniqueId id;
+    RCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(id) == 128, "nccl unique id size");
+    std::memcpy(out128, &id, sizeof id);
+    return XH_OK;
+  });
+}
+
+int xh_ctx_create(int device, int rank, int world, const void *uid128,
+                  xh_ctx **out) {
+  return guard([&]() -> int {
+    if (!out) return fail(XH_ERR_INVALID, "null out");
+    if (world < 1 || rank < 0 || rank >= world)
+      return fail(XH_ERR_INVALID, "bad rank %d / world %d", rank, world);
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+      return fail(XH_ERR_INVALID, "device %d of %d", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    auto *c = new xh_ctx;
+    c->device = device;
+    c->rank = rank;
+    c->world = world;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(XH_ERR_HIP, "stream: %s", hipGetErrorString(e));
+    }
+    if (world > 1) {
+      if (!uid128) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return fail(XH_ERR_INVALID, "world > 1 needs the RCCL unique id");
+      }
+      ncclUniqueId id;
+      std::memcpy(&id, uid128, sizeof id);
+      ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+      if (r != ncclSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return fail(XH_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+      }
+    }
+    *out = c;
+    return XH_OK;
+  });
+}
+
+int xh_ctx_destroy(xh_ctx *c) {
+  return guard([&]() -> int {
+    if (!c) return XH_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return XH_OK;
+  });
+}
+
+int xh_ctx_synchronize(xh_ctx *c) {
+  return guard([&]() -> int {
+    if (!c) return fail(XH_ERR_INVALID, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return XH_OK;
+  });
+}
+
+int xh_ctx_allreduce_host(xh_ctx *c, float *data, size_t n) {
+  return guard([&]() -> int {
+    if (!c || (!data && n)) return fail(XH_ERR_INVALID, "null arg");
+    if (c->world <= 1 || n == 0) return XH_OK;
+    float *d = nullptr;
+    HIPCHK(hipMalloc(&d, n * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(d, data, n * sizeof(float), hipMemcpyHostToDevice,
+                          c->stream));
+    RCCLCHK(ncclAllReduce(d, d, n, ncclFloat32, ncclSum, c->comm, c->stream));
+    HIPCHK(hipMemcpyAsync(data, d, n * sizeof(float), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(d));
+    return XH_OK;
+  });
+}
+
+void xh_config_default(xh_config *c, int algo, int bins, int dims, int num_envs,
+                       int steps) {
+  std::memset(c, 0, sizeof *c);
+  c->algo = algo;
+  c->num_envs = c->num_envs_global = num_envs;
+  c->env_offset = 0;
+  c->bins = bins;
+  c->dims = dims;
+  c->steps = steps;
+  c->epochs = algo == XH_PPO ? 4 : 1;
+  c->policy_h1 = 128;
+  c->policy_h2 = algo == XH_PPO ? 64 : 32;
+  if (algo == XH_AC) c->policy_h1 = 64;
+  c->value_h1 = 64;
+  c->value_h2 = 32;
+  // ppo_training.cc:17,26 / ac_training.cc:17,26
+  c->lr_policy = algo == XH_PPO ? 1e-4f : 1e-5f;
+  c->lr_value = algo == XH_PPO ? 1e-5f : 1e-4f;
+  c->gamma = 0.99f;
+  c->lambda = 0.95f;
+  c->clip_eps = 0.2f;
+  c->rng_state = 1;
+}
+
+int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
+  return guard([&]() -> int {
+    if (!ctx || !cfg || !out) return fail(XH_ERR_INVALID, "null arg");
+    const xh_config &c = *cfg;
+    if (c.algo != XH_PPO && c.algo != XH_AC)
+      return fail(XH_ERR_INVALID, "algo %d", c.algo);
+    if (!xh::policy_shape_supported(c.bins, c.dims, c.policy_h1, c.policy_h2))
+      return fail(XH_ERR_INVALID,
+                  "unsupported policy shape B=%d D=%d widths=[%d,%d]", c.bins,
+                  c.dims, c.policy_h1, c.policy_h2);
+    if (!xh::value_shape_supported(c.value_h1, c.value_h2))
+      return fail(XH_ERR_INVALID, "unsupported value widths [%d,%d]",
+                  c.value_h1, c.value_h2);
+    const int G = 64 / c.bins;
+    if (c.num_envs <= 0 || c.num_envs % G)
+      return fail(XH_ERR_INVALID, "num_envs %d must be a positive multiple of %d",
+                  c.num_envs, G);
+    if (c.steps < 1 || c.steps > 64)
+      return fail(XH_ERR_INVALID, "steps %d not in [1,64]", c.steps);
+    if (c.epochs < 1 || c.epochs > 64)
+      return fail(XH_ERR_INVALID, "epochs %d", c.epochs);
+    if (c.num_envs_global < c.num_envs || c.env_offset < 0 ||
+        c.env_offset + c.num_envs > c.num_envs_global)
+      return fail(XH_ERR_INVALID, "env partition offset %d + %d > global %d",
+                  c.env_offset, c.num_envs, c.num_envs_global);
+    if (c.bins * 2 * c.dims > 768)
+      return fail(XH_ERR_INVALID, "value input %d > 768", c.bins * 2 * c.dims);
+    HIPCHK(hipSetDevice(ctx->device));
+
+    auto *t = new xh_trainer;
+    t->ctx = ctx;
+    t->cfg = c;
+    // minstd_rand0 seeding rule: s mod m, 0 -> 1
+    t->cfg.rng_state = c.rng_state % 2147483647u;
+    if (t->cfg.rng_state == 0) t->cfg.rng_state = 1;
+    static const int ia[3][3] = {{4, 0, 0}, {4, 2, 0}, {4, 2, 2}};
+    static const int ib[3][3] = {{1, 0, 0}, {1, 2, 0}, {1, 2, 1}};
+    t->env.B = c.bins;
+    t->env.D = c.dims;
+    for (int d = 0; d < 3; ++d) {
+      t->env.item_a[d] = ia[c.dims - 1][d];
+      t->env.item_b[d] = ib[c.dims - 1][d];
+    }
+    t->env.p_a = 0.4;
+    t->pl = xh::PolicyLayout{2 * c.dims, c.policy_h1, c.policy_h2};
+    t->vl = xh::ValueLayout{c.bins * 2 * c.dims, c.value_h1, c.value_h2};
+    t->np = t->pl.size();
+    t->nv = t->vl.size();
+    const size_t N = t->N(), T = t->T();
+    int st = XH_OK;
+    auto A = [&](auto **p, size_t bytes) {
+      if (st == XH_OK) st = dalloc(t, p, bytes);
+    };
+    A(&t->bins, (T + 1) * N * t->BD());
+    A(&t->items, (T + 1) * N * 4);
+    A(&t->action, T * N * 4);
+    A(&t->forced, T * N * 4);
+    A(&t->pold, T * N * 4);
+    A(&t->done, T * N);
+    A(&t->rng, N * 4);
+    A(&t->pp, (size_t)t->np * 4);
+    A(&t->vp, (size_t)t->nv * 4);
+    A(&t->vw1t, (size_t)t->vl.V1 * t->vl.Fin * 4);
+    A(&t->v_state, (T + 1) * N * 4);
+    A(&t->v_state0, (T + 1) * N * 4);
+    A(&t->v_term, T * N * 4);
+    A(&t->targets, T * N * 4);
+    A(&t->adv, T * N * 4);
+    A(&t->row_g, T * N * 4);
+    A(&t->row_h1, T * N * c.value_h1 * 4);
+    A(&t->row_h2, T * N * c.value_h2 * 4);
+    A(&t->row_d1, T * N * c.value_h1 * 4);
+    A(&t->row_d2, T * N * c.value_h2 * 4);
+    t->rgrid = xh::rollout_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
+    t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
+    const int groups = (int)(T * N / (size_t)G);
+    if (t->pslab_n > groups) t->pslab_n = groups;
+    t->pslab_stride = (t->np + 63) & ~63;
+    t->vslab_n = 256;
+    const long vrows = (long)T * N;
+    if (t->vslab_n > vrows) t->vslab_n = (int)vrows;
+    t->vslab_stride = (t->nv + 63) & ~63;
+    A(&t->pslab, (size_t)t->pslab_n * t->pslab_stride * 4);
+    A(&t->vslab, (size_t)t->vslab_n * t->vslab_stride * 4);
+    A(&t->pgrads, (size_t)c.epochs * t->np * 4);
+    A(&t->vgrad, (size_t)t->nv * 4);
+    A(&t->logits, N * c.bins * 4);
+    A(&t->probs, N * c.bins * 4);
+    if (st != XH_OK) {
+      std::string keep = g_err;
+      xh_trainer_destroy(t);
+      g_err = keep;
+      return st;
+    }
+    // a^(4T(Ng-1)): from this env's last draw of an iteration to its next.
+    t->jump_mul = mstd_pow(4ull * T * (uint64_t)(c.num_envs_global - 1));
+    hipError_t e = xh::launch_env_init(t->env, t->batch(), t->cfg.rng_state,
+                                       c.env_offset, c.num_envs_global,
+                                       ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      xh_trainer_destroy(t);
+      return fail(XH_ERR_HIP, "env init: %s", hipGetErrorString(e));
+    }
+    *out = t;
+    return XH_OK;
+  });
+}
+
+int xh_trainer_destroy(xh_trainer *t) {
+  return guard([&]() -> int {
+    if (!t) return XH_OK;
+    hipSetDevice(t->ctx->device);
+    hipStreamSynchronize(t->ctx->stream);
+    for (auto &ev : t->events) {
+      hipEventDestroy(ev.start);
+      hipEventDestroy(ev.stop);
+    }
+    for (void *p : t->allocs) hipFree(p);
+    delete t;
+    return XH_OK;
+  });
+}
+
+size_t xh_trainer_num_params(const xh_trainer *t, int which) {
+  if (!t) return 0;
+  return which == XH_POLICY ? (size_t)t->np : (size_t)t->nv;
+}
+
+int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
+                          size_t n) {
+  return guard([&]() -> int {
+    if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
+    const size_t want = xh_trainer_num_params(t, which);
+    if (n != want)
+      return fail(XH_ERR_INVALID, "params: got %zu floats, model has %zu", n,
+                  want);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    float *dst = which == XH_POLICY ? t->pp : t->vp;
+    HIPCHK(hipMemcpyAsync(dst, host, n * 4, hipMemcpyHostToDevice,
+                          t->ctx->stream));
+    if (which == XH_VALUE) CHK(refresh_value_transpose(t));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    return XH_OK;
+  });
+}
+
+int xh_trainer_get_params(xh_trainer *t, int which, float *host, size_t n) {
+  return guard([&]() -> int {
+    if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
+    const size_t want = xh_trainer_num_params(t, which);
+    if (n != want)
+      return fail(XH_ERR_INVALID, "params: got %zu floats, model has %zu", n,
+                  want);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    HIPCHK(hipMemcpyAsync(host, which == XH_POLICY ? t->pp : t->vp, n * 4,
+                          hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    return XH_OK;
+  });
+}
+
+int xh_trainer_rollout(xh_trainer *t) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    HIPCHK(hipSetDevice(t->ctx->device));
+    return do_rollout(t);
+  });
+}
+
+int xh_trainer_learn(xh_trainer *t) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    HIPCHK(hipSetDevice(t->ctx->device));
+    return do_learn(t);
+  });
+}
+
+int xh_trainer_iterate(xh_trainer *t, int iterations) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    HIPCHK(hipSetDevice(t->ctx->device));
+    for (int i = 0; i < iterations; ++i) {
+      CHK(do_rollout(t));
+      CHK(do_learn(t));
+    }
+    return XH_OK;
+  });
+}
+
+int xh_trainer_set_forced_actions(xh_trainer *t, const int32_t *host) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    if (!host) {
+      t->use_forced = false;
+      return XH_OK;
+    }
+    const size_t n = t->T() * t->N();
+    for (size_t i = 0; i < n; ++i)
+      if (host[i] < 0 || host[i] >= t->cfg.bins)
+        return fail(XH_ERR_INVALID, "forced action %d out of range", host[i]);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    HIPCHK(hipMemcpyAsync(t->forced, host, n * 4, hipMemcpyHostToDevice,
+                          t->ctx->stream));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    t->use_forced = true;
+    return XH_OK;
+  });
+}
+
+size_t xh_trainer_buffer_bytes(const xh_trainer *t, int which) {
+  return t ? buffer_bytes(t, which) : 0;
+}
+
+int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes) {
+  return guard([&]() -> int {
+    if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
+    const size_t want = buffer_bytes(t, which);
+    if (!want || bytes != want)
+      return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
+                  bytes, want);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    HIPCHK(hipMemcpyAsync(host, buffer_ptr(t, which), bytes,
+                          hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    return XH_OK;
+  });
+}
+
+int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
+                          size_t bytes) {
+  return guard([&]() -> int {
+    if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
+    const size_t want = buffer_bytes(t, which);
+    if (!want || bytes != want)
+      return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
+                  bytes, want);
+    if (which == XH_BUF_ACTION) {
+      const int32_t *a = static_cast<const int32_t *>(host);
+      for (size_t i = 0; i < bytes / 4; ++i)
+        if (a[i] < 0 || a[i] >= t->cfg.bins)
+          return fail(XH_ERR_INVALID, "action %d out of range", a[i]);
+    }
+    HIPCHK(hipSetDevice(t->ctx->device));
+    HIPCHK(hipMemcpyAsync(buffer_ptr(t, which), host, bytes,
+                          hipMemcpyHostToDevice, t->ctx->stream));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    if (which == XH_BUF_BINS || which == XH_BUF_ITEMS) t->need_shift = false;
+    return XH_OK;
+  });
+}
+
+int xh_trainer_set_timing(xh_trainer *t, int on) {
+  if (!t) return fail(XH_ERR_INVALID, "null trainer");
+  t->timing = on != 0;
+  return XH_OK;
+}
+
+int xh_trainer_reset_timing(xh_trainer *t) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    for (auto &ev : t->events) {
+      hipEventDestroy(ev.start);
+      hipEventDestroy(ev.stop);
+    }
+    t->events.clear();
+    return XH_OK;
+  });
+}
+
+int xh_trainer_kernel_time(xh_trainer *t, const char *name, double *ms,
+                           long *launches) {
+  return guard([&]() -> int {
+    if (!t || !name || !ms || !launches) return fail(XH_ERR_INVALID, "null arg");
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    double total = 0;
+    long n = 0;
+    for (auto &ev : t->events) {
+      if (ev.name != name) continue;
+      float e = 0;
+      HIPCHK(hipEventElapsedTime(&e, ev.start, ev.stop));
+      total += e;
+      ++n;
+    }
+    *ms = total;
+    *launches = n;
+    return XH_OK;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+"""Python host wrapper over the C ABI: one process per GPU.
+
+Mirrors the reference's learner vocabulary (xylo/policy_gradient.h,
+apps/bin_packing/bin_packing.h) for the vectorised path:
+
+    ctx = Context(device=0)
+    tr = Trainer(ctx, algo="ppo", bins=64, dims=2, num_envs=32768, steps=4,
+                 widths=(128, 128))
+    tr.set_params(POLICY, w); tr.set_params(VALUE, v)
+    tr.iterate(10)           # 10 x (agents.play_steps(T); learner.step())
+
+All arrays crossing this wrapper are numpy host copies; the hot loop never
+leaves the device.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (BUF_ACTION, BUF_ADV, BUF_BINS, BUF_DONE, BUF_ITEMS,
+                   BUF_LOGITS, BUF_POLD, BUF_POLICY_GRADS, BUF_PROBS, BUF_RNG,
+                   BUF_TARGETS, BUF_V_STATE, BUF_V_STATE0, BUF_V_TERM,
+                   BUF_VALUE_GRAD, XH_AC, XH_POLICY, XH_PPO, XH_VALUE, check)
+
+POLICY, VALUE = XH_POLICY, XH_VALUE
+ALGOS = {"ppo": XH_PPO, "ac": XH_AC}
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """xh_ctx: a device, its stream and (world > 1) an RCCL communicator."""
+
+    def __init__(self, device=0, rank=0, world=1, uid=None):
+        self.h = C.c_void_p()
+        buf = None
+        if uid is not None:
+            buf = (C.c_char * 128).from_buffer_copy(bytes(uid))
+        check(_lib.lib.xh_ctx_create(device, rank, world,
+                                     C.cast(buf, C.c_void_p) if buf else None,
+                                     C.byref(self.h)))
+        self.device, self.rank, self.world = device, rank, world
+
+    @staticmethod
+    def unique_id():
+        out = (C.c_char * 128)()
+        check(_lib.lib.xh_comm_unique_id(out))
+        return bytes(out)
+
+    def synchronize(self):
+        check(_lib.lib.xh_ctx_synchronize(self.h))
+
+    def allreduce_host(self, arr):
+        a = np.ascontiguousarray(arr, np.float32).copy()
+        check(_lib.lib.xh_ctx_allreduce_host(self.h, _ptr(a), a.size))
+        return a
+
+    def close(self):
+        if self.h:
+            check(_lib.lib.xh_ctx_destroy(self.h))
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def policy_param_count(dims, h1, h2):
+    f0 = 2 * dims
+    return h1 * f0 + h1 + h2 * h1 + h2 + h2 + 1
+
+
+def value_param_count(bins, dims, v1=64, v2=32):
+    fin = bins * 2 * dims
+    return v1 * fin + v1 + v2 * v1 + v2 + v2 + 1
+
+
+def init_policy(dims, h1, h2, seed=0):
+    """Reference initialisation scheme for conv1d_1 layers: weights
+    N(0, sqrt(2/fan_in)) (he_initialize, nn.h:16-18,123), biases 0.  Drawn
+    with numpy (distribution-equal, not stream-equal to the reference)."""
+    rng = np.random.default_rng(seed)
+    f0 = 2 * dims
+    parts = []
+    for fi, fo in ((f0, h1), (h1, h2), (h2, 1)):
+        parts.append(rng.normal(0.0, np.sqrt(2.0 / fi), fo * fi))
+        parts.append(np.zeros(fo))
+    return np.concatenate(parts).astype(np.float32)
+
+
+def init_value(bins, dims, v1=64, v2=32, seed=1):
+    """full_layer init N(0, 0.01) (normal_initialize, nn.h:12-14,68)."""
+    rng = np.random.default_rng(seed)
+    fin = bins * 2 * dims
+    parts = []
+    for fi, fo in ((fin, v1), (v1, v2), (v2, 1)):
+        parts.append(rng.normal(0.0, 0.01, fo * fi))
+        parts.append(np.zeros(fo))
+    return np.concatenate(parts).astype(np.float32)
+
+
+class Trainer:
+    """xh_trainer: N vectorised bin-packing envs + per-bin policy + value net +
+    PPO (ppo_learner) or actor-critic (actor_critic_learner) learner."""
+
+    def __init__(self, ctx, algo="ppo", bins=64, dims=2, num_envs=4096, steps=4,
+                 widths=(128, 128), value_widths=(64, 32), epochs=None,
+                 lr_policy=None, lr_value=None, wd_policy=0.0, wd_value=0.0,
+                 gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
+                 num_envs_global=None, env_offset=0):
+        cfg = _lib.Config()
+        a = ALGOS[algo]
+        _lib.lib.xh_config_default(C.byref(cfg), a, bins, dims, num_envs, steps)
+        cfg.num_envs_global = num_envs_global or num_envs
+        cfg.env_offset = env_offset
+        cfg.policy_h1, cfg.policy_h2 = widths
+        cfg.value_h1, cfg.value_h2 = value_widths
+        if epochs is not None:
+            cfg.epochs = epochs
+        if lr_policy is not None:
+            cfg.lr_policy = lr_policy
+        if lr_value is not None:
+            cfg.lr_value = lr_value
+        cfg.wd_policy, cfg.wd_value = wd_policy, wd_value
+        cfg.gamma, cfg.lambda_, cfg.clip_eps = gamma, lam, clip_eps
+        cfg.rng_state = rng_state
+        self.cfg = cfg
+        self.ctx = ctx
+        self.B, self.D, self.N, self.T = bins, dims, num_envs, steps
+        self.epochs = cfg.epochs
+        self.h = C.c_void_p()
+        check(_lib.lib.xh_trainer_create(ctx.h, C.byref(cfg), C.byref(self.h)))
+        self.np_ = _lib.lib.xh_trainer_num_params(self.h, POLICY)
+        self.nv = _lib.lib.xh_trainer_num_params(self.h, VALUE)
+
+    # ------------------------------------------------------------ params --
+    def num_params(self, which):
+        return self.np_ if which == POLICY else self.nv
+
+    def set_params(self, which, p):
+        p = np.ascontiguousarray(p, np.float32)
+        check(_lib.lib.xh_trainer_set_params(self.h, which, _ptr(p), p.size))
+
+    def params(self, which):
+        out = np.zeros(self.num_params(which), np.float32)
+        check(_lib.lib.xh_trainer_get_params(self.h, which, _ptr(out), out.size))
+        return out
+
+    # -------------------------------------------------------------- loop --
+    def rollout(self):
+        check(_lib.lib.xh_trainer_rollout(self.h))
+
+    def learn(self):
+        check(_lib.lib.xh_trainer_learn(self.h))
+
+    def iterate(self, n=1):
+        check(_lib.lib.xh_trainer_iterate(self.h, n))
+
+    def synchronize(self):
+        self.ctx.synchronize()
+
+    def set_forced_actions(self, actions):
+        if actions is None:
+            check(_lib.lib.xh_trainer_set_forced_actions(self.h, None))
+            return
+        a = np.ascontiguousarray(actions, np.int32).reshape(self.T, self.N)
+        check(_lib.lib.xh_trainer_set_forced_actions(self.h, _ptr(a)))
+
+    # ----------------------------------------------------------- buffers --
+    def _spec(self, which):
+        T, N, B, D = self.T, self.N, self.B, self.D
+        return {
+            BUF_BINS: (np.int8, (T + 1, N, B, D)),
+            BUF_ITEMS: (np.int8, (T + 1, N, 4)),
+            BUF_ACTION: (np.int32, (T, N)),
+            BUF_POLD: (np.float32, (T, N)),
+            BUF_DONE: (np.uint8, (T, N)),
+            BUF_RNG: (np.uint32, (N,)),
+            BUF_V_STATE: (np.float32, (T + 1, N)),
+            BUF_V_STATE0: (np.float32, (T + 1, N)),
+            BUF_V_TERM: (np.float32, (T, N)),
+            BUF_TARGETS: (np.float32, (T, N)),
+            BUF_ADV: (np.float32, (T, N)),
+            BUF_VALUE_GRAD: (np.float32, (self.nv,)),
+            BUF_POLICY_GRADS: (np.float32, (self.epochs, self.np_)),
+            BUF_LOGITS: (np.float32, (N, B)),
+            BUF_PROBS: (np.float32, (N, B)),
+        }[which]
+
+    def buffer(self, which):
+        dt, shape = self._spec(which)
+        out = np.zeros(shape, dt)
+        check(_lib.lib.xh_trainer_get_buffer(self.h, which, _ptr(out), out.nbytes))
+        return out
+
+    def set_buffer(self, which, arr):
+        dt, shape = self._spec(which)
+        a = np.ascontiguousarray(arr, dt).reshape(shape)
+        check(_lib.lib.xh_trainer_set_buffer(self.h, which, _ptr(a), a.nbytes))
+
+    # ------------------------------------------------------------ timing --
+    def set_timing(self, on):
+        check(_lib.lib.xh_trainer_set_timing(self.h, 1 if on else 0))
+
+    def reset_timing(self):
+        check(_lib.lib.xh_trainer_reset_timing(self.h))
+
+    def kernel_time(self, name):
+        ms, n = C.c_double(), C.c_long()
+        check(_lib.lib.xh_trainer_kernel_time(self.h, name.encode(), C.byref(ms),
+                                              C.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if self.h:
+            check(_lib.lib.xh_trainer_destroy(self.h))
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,143 @@
+/* xylo_hip.h -- C ABI of the MI355X-native PPO / actor-critic hot path.
+ *
+ * The drop-in boundary for the rollout-and-update path of
+ * beehover/dependence_free_rl (reference @ 2024_10_08; citations are
+ * file:line under that tree).  Plain pointers, sizes and int status codes;
+ * no C++ or torch types cross this boundary; no exception escapes it.
+ * Host wrappers (include/xylo_hip/ headers, dependence_free_rl_amd/_lib.py)
+ * rethrow / raise on a non-zero status with xh_last_error().
+ *
+ * Reference interfaces replaced (one xh_trainer = many envs + the learner):
+ *   xylo::environment<A,S>::apply/view/reset   xylo/rl.h:163-170
+ *   bp::environment, bp::agent                 apps/bin_packing/bin_packing.h:46-107
+ *   xylo::agent::step / play_steps             xylo/rl.h:325-360
+ *   xylo::replay_buffer (sample_td, forget)    xylo/rl.h:213-296
+ *   xylo::policy_gradient_policy::react        xylo/policy_gradient.h:337-354
+ *   xylo::discrete_action::from_vector         xylo/rl.h:27-30
+ *   xylo::actor_critic_learner::learn          xylo/policy_gradient.h:159-281
+ *   xylo::ppo_learner::optimize_action         xylo/policy_gradient.h:297-307
+ *   xylo::model::parameters / set_parameters   xylo/nn.h:490-508
+ *   xylo::sgd_optimizer                        xylo/nn.h:616-628
+ *   (and the tensor.{h,cc} / nn.h Dense, relu, softmax loops underneath)
+ */
+#ifndef XYLO_HIP_H_
+#define XYLO_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------ status ---- */
+enum {
+  XH_OK = 0,
+  XH_ERR_INVALID = 1,     /* bad argument / unsupported shape   */
+  XH_ERR_HIP = 2,         /* HIP runtime error                   */
+  XH_ERR_RCCL = 3,        /* RCCL error                          */
+  XH_ERR_STATE = 4        /* call out of order                   */
+};
+/* Message of the last failing call on this thread ("" if none). */
+const char *xh_last_error(void);
+/* Library version string. */
+const char *xh_version(void);
+
+/* ------------------------------------------------------------ context --- */
+typedef struct xh_ctx xh_ctx;
+/* 128-byte RCCL unique id (ncclGetUniqueId) for a world > 1 job. */
+int xh_comm_unique_id(void *out128);
+/* device: HIP device ordinal; rank/world: this process in a one-process-per-
+ * GPU job; uid128 (world > 1): the id from rank 0, broadcast by the caller. */
+int xh_ctx_create(int device, int rank, int world, const void *uid128,
+                  xh_ctx **out);
+int xh_ctx_destroy(xh_ctx *ctx);
+int xh_ctx_synchronize(xh_ctx *ctx);
+/* Sum-all-reduce of n floats of host memory over the job (tests/tools). */
+int xh_ctx_allreduce_host(xh_ctx *ctx, float *data, size_t n);
+
+/* ------------------------------------------------------------ trainer --- */
+enum { XH_PPO = 0, XH_AC = 1 };
+
+typedef struct {
+  int algo;            /* XH_PPO (ppo_learner) | XH_AC (actor_critic_learner) */
+  int num_envs;        /* envs on this rank (multiple of 64/bins)            */
+  int num_envs_global; /* envs in the whole job (reference-order RNG streams) */
+  int env_offset;      /* global index of this rank's first env              */
+  int bins, dims;      /* B (bin_packing.h:12 num_bins), D (2 in the ref)    */
+  int steps;           /* T: env steps per env per iteration (play_steps(T)) */
+  int epochs;          /* PPO k (policy_gradient.h:300), 1 for AC            */
+  int policy_h1, policy_h2; /* per-bin conv1d_1 widths                       */
+  int value_h1, value_h2;   /* value full_layer widths (64, 32)              */
+  float lr_policy, lr_value, wd_policy, wd_value;
+  float gamma;         /* 0.99 */
+  float lambda;        /* 0.95 (policy_gradient.h:286) */
+  float clip_eps;      /* 0.2  (rl.h:56) */
+  uint32_t rng_state;  /* minstd_rand0 state before the envs are constructed */
+} xh_config;
+
+/* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */
+void xh_config_default(xh_config *c, int algo, int bins, int dims, int num_envs,
+                       int steps);
+
+typedef struct xh_trainer xh_trainer;
+/* Allocates all device buffers, constructs the envs (2 engine draws each,
+ * bin_packing.h:50-52) and zero-initialises both nets (set params next). */
+int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out);
+int xh_trainer_destroy(xh_trainer *t);
+
+enum { XH_POLICY = 0, XH_VALUE = 1 };
+/* Flat parameters in the reference model::parameters() layout (nn.h:499-508):
+ * per dense layer [A(out x in) row-major, b(out)]; weights.20 loads as-is. */
+size_t xh_trainer_num_params(const xh_trainer *t, int which);
+int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
+                          size_t n);
+int xh_trainer_get_params(xh_trainer *t, int which, float *host, size_t n);
+
+/* One iteration's rollout: T steps of every env (one kernel per step). */
+int xh_trainer_rollout(xh_trainer *t);
+/* learn(): value step, advantages, `epochs` policy steps; then the batch's
+ * final states become the next iteration's starting states (forget()). */
+int xh_trainer_learn(xh_trainer *t);
+/* `iterations` x (rollout + learn), asynchronous on the trainer's stream. */
+int xh_trainer_iterate(xh_trainer *t, int iterations);
+/* Teacher forcing: actions [T][N] used instead of sampling (the sampler's two
+ * engine draws are still consumed).  NULL disables. */
+int xh_trainer_set_forced_actions(xh_trainer *t, const int32_t *host);
+
+/* Batch / diagnostics buffers (host copies; sizes in bytes must match). */
+enum {
+  XH_BUF_BINS = 0,     /* int8  [T+1][N][B][D]  states S_t (slot T = next S_0) */
+  XH_BUF_ITEMS = 1,    /* int8  [T+1][N][4]                                  */
+  XH_BUF_ACTION = 2,   /* int32 [T][N]                                       */
+  XH_BUF_POLD = 3,     /* f32   [T][N]  distrib[choice] at sampling          */
+  XH_BUF_DONE = 4,     /* uint8 [T][N]                                       */
+  XH_BUF_RNG = 5,      /* uint32 [N]   per-env engine state                  */
+  XH_BUF_V_STATE = 6,  /* f32   [T+1][N] V(S_t) of the last value eval       */
+  XH_BUF_V_TERM = 7,   /* f32   [T][N]  V(terminal view of step t)           */
+  XH_BUF_TARGETS = 8,  /* f32   [T][N]  TD targets                           */
+  XH_BUF_ADV = 9,      /* f32   [T][N]  advantages                           */
+  XH_BUF_VALUE_GRAD = 10,  /* f32 [value params]  last value gradient        */
+  XH_BUF_POLICY_GRADS = 11,/* f32 [epochs][policy params]                    */
+  XH_BUF_LOGITS = 12,  /* f32   [N][B]  logits of the last rollout step      */
+  XH_BUF_PROBS = 13,   /* f32   [N][B]  probabilities of the last step       */
+  XH_BUF_V_STATE0 = 14,/* f32   [T+1][N] V(S_t) before the value step        */
+  XH_BUF_COUNT
+};
+size_t xh_trainer_buffer_bytes(const xh_trainer *t, int which);
+int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes);
+int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
+                          size_t bytes);
+
+/* Kernel timing with HIP events on the trainer's stream (off by default). */
+int xh_trainer_set_timing(xh_trainer *t, int on);
+/* name: "rollout_step" | "policy_train" | "value" | "reduce_sgd" | "allreduce"
+ * Returns accumulated milliseconds and launch count since the last reset. */
+int xh_trainer_kernel_time(xh_trainer *t, const char *name, double *ms,
+                           long *launches);
+int xh_trainer_reset_timing(xh_trainer *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XYLO_HIP_H_ */

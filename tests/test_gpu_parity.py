@@ -1,0 +1,159 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors of
+the real reference and against the CPU oracle.  Run on the MI355X box:
+
+    python -m pytest tests -m gpu -x -q
+
+Bit-exact: env states, items, dones, actions, RNG states.  Tolerance
+(|x - y| <= 1e-4 * max(1, |y|), conftest.RTOL): logits, probabilities,
+values, advantages, gradients, parameters.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_close, golden
+from gpu_helpers import meta, row_index, step_major, trainer_from_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch  # noqa: F401  (device discovery only; no torch compute)
+    from dependence_free_rl_amd import Context
+    c = Context(device=0)
+    yield c
+    c.close()
+
+
+ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2"]
+
+
+@pytest.mark.parametrize("name", ENV_CASES)
+def test_env_construction_bit_exact(ctx, name):
+    from dependence_free_rl_amd.trainer import BUF_BINS, BUF_ITEMS
+    tr, g, kv = trainer_from_golden(ctx, name)
+    N, T, D = tr.N, tr.T, tr.D
+    bins = tr.buffer(BUF_BINS)[0]
+    items = tr.buffer(BUF_ITEMS)[0, :, :D]
+    s_bins = step_major(g["it0_step_bins"], N, T)[0]
+    s_item = step_major(g["it0_step_item"], N, T)[0]
+    np.testing.assert_array_equal(bins, s_bins)
+    np.testing.assert_array_equal(items, s_item)
+
+
+@pytest.mark.parametrize("name", ENV_CASES)
+def test_rollout_teacher_forced_bit_exact(ctx, name):
+    """Given the reference's actions, every env transition, item draw, reset
+    and RNG state matches the reference bit for bit."""
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd.trainer import (BUF_BINS, BUF_DONE, BUF_ITEMS,
+                                                BUF_POLD, BUF_RNG, POLICY)
+    tr, g, kv = trainer_from_golden(ctx, name)
+    N, T, B, D = tr.N, tr.T, tr.B, tr.D
+    x0 = int(g["x0"][0])
+    for it in range(int(kv["iters"])):
+        p = "it%d_" % it
+        if it > 0:
+            tr.set_params(POLICY, g["it%d_policy_params" % (it - 1)])
+        tr.set_forced_actions(step_major(g[p + "step_choice"], N, T))
+        tr.rollout()
+        bins = tr.buffer(BUF_BINS)
+        np.testing.assert_array_equal(bins[:T], step_major(g[p + "step_bins"], N, T))
+        np.testing.assert_array_equal(bins[T], g[p + "final_bins"])
+        items = tr.buffer(BUF_ITEMS)[:, :, :D]
+        np.testing.assert_array_equal(items[:T], step_major(g[p + "step_item"], N, T))
+        np.testing.assert_array_equal(items[T], g[p + "final_item"])
+        np.testing.assert_array_equal(tr.buffer(BUF_DONE),
+                                      step_major(g[p + "step_done"], N, T))
+        dist = g[p + "step_distrib"]
+        pch = dist[np.arange(len(dist)), g[p + "step_choice"]]
+        assert_close(tr.buffer(BUF_POLD), step_major(pch, N, T), what="p_old")
+        # per-env engine states: reference-order positions
+        rng = tr.buffer(BUF_RNG)
+        for e in (0, N - 1):
+            pos = 2 * N + 4 * T * N * (it + 1) + 4 * T * e
+            assert rng[e] == po.minstd_jump(x0, pos)
+        assert po.minstd_jump(int(g[p + "x_end"][0]), 4 * T * (N - 1)) == rng[N - 1]
+        tr.learn()  # advance the batch window (forget())
+
+
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "ppo_b64d2"])
+def test_rollout_sampling_matches_reference(ctx, name):
+    """Free-running: the GPU's own softmax + categorical sampler picks the
+    reference's actions (no fixture step lies on a probability near-tie)."""
+    from dependence_free_rl_amd.trainer import BUF_ACTION, BUF_BINS, POLICY, VALUE
+    tr, g, kv = trainer_from_golden(ctx, name)
+    N, T = tr.N, tr.T
+    for it in range(int(kv["iters"])):
+        p = "it%d_" % it
+        if it > 0:  # re-sync parameters so only sampling is under test
+            tr.set_params(POLICY, g["it%d_policy_params" % (it - 1)])
+            tr.set_params(VALUE, g["it%d_value_params" % (it - 1)])
+        tr.rollout()
+        np.testing.assert_array_equal(tr.buffer(BUF_ACTION),
+                                      step_major(g[p + "step_choice"], N, T))
+        np.testing.assert_array_equal(tr.buffer(BUF_BINS)[T], g[p + "final_bins"])
+        tr.learn()
+
+
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2"])
+def test_learn_matches_reference(ctx, name):
+    """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
+    value gradient and updated parameters vs the reference learner."""
+    from dependence_free_rl_amd.trainer import (BUF_ADV, BUF_POLICY_GRADS,
+                                                BUF_V_STATE0, BUF_V_TERM,
+                                                BUF_VALUE_GRAD, POLICY, VALUE)
+    tr, g, kv = trainer_from_golden(ctx, name)
+    N, T = tr.N, tr.T
+    worst = {}
+    for it in range(int(kv["iters"])):
+        p = "it%d_" % it
+        tr.set_forced_actions(step_major(g[p + "step_choice"], N, T))
+        tr.rollout()
+        tr.learn()
+        rows = row_index(g, it, T)
+        v0, vt, adv = tr.buffer(BUF_V_STATE0), tr.buffer(BUF_V_TERM), tr.buffer(BUF_ADV)
+        vrow, arow = [], []
+        for kind, t, e in rows:
+            if kind == 0:
+                vrow.append(v0[t, e]); arow.append(adv[t, e])
+            elif kind == 1:
+                vrow.append(v0[T, e]); arow.append(0.0)
+            else:
+                vrow.append(vt[t, e]); arow.append(0.0)
+        checks = [
+            ("values", np.array(vrow), g[p + "values_before"]),
+            ("advantages", np.array(arow), g[p + "advantages"]),
+            ("value_grad", tr.buffer(BUF_VALUE_GRAD), g[p + "value_grad"]),
+            ("value_params", tr.params(VALUE), g[p + "value_params"]),
+            ("policy_grads", tr.buffer(BUF_POLICY_GRADS), g[p + "policy_grads"]),
+            ("policy_params", tr.params(POLICY), g[p + "policy_params"]),
+        ]
+        for what, x, y in checks:
+            worst[what] = max(worst.get(what, 0.0),
+                              assert_close(x, y, what=p + what))
+    print(name, {k: "%.2e" % v for k, v in worst.items()})
+
+
+def test_weights20_logits(ctx):
+    """deep_agent.cc's trained policy (weights.20): GPU logits vs the
+    reference's model::eval for 64 fixed observations."""
+    from dependence_free_rl_amd import Trainer
+    from dependence_free_rl_amd.trainer import (BUF_BINS, BUF_ITEMS, BUF_LOGITS,
+                                                POLICY)
+    g = golden("deep_w20")
+    tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=64, steps=1,
+                 widths=(128, 64))
+    tr.set_params(POLICY, g["params"])
+    obs = g["obs"].reshape(64, 8, 4)
+    bins = np.zeros((2, 64, 8, 2), np.int8)
+    bins[0] = np.rint(obs[:, :, :2] * 8).astype(np.int8)
+    items = np.zeros((2, 64, 4), np.int8)
+    items[0, :, :2] = np.rint(obs[:, 0, 2:] * 8).astype(np.int8)
+    tr.set_buffer(BUF_BINS, bins)
+    tr.set_buffer(BUF_ITEMS, items)
+    tr.set_forced_actions(np.zeros((1, 64), np.int32))
+    tr.rollout()
+    z = tr.buffer(BUF_LOGITS)
+    assert_close(z, g["logits"], what="weights.20 logits")
+    assert abs(z[0, 0] - 2.76766) < 1e-4 and np.allclose(z[0], z[0, 0], atol=1e-6)

@@ -1,0 +1,131 @@
+"""GPU vs CPU oracle at the benchmark shape (64 bins, 2-D, [128,128]) and
+size-independent properties at the full BASELINE config-3 size."""
+import numpy as np
+import pytest
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch  # noqa: F401
+    from dependence_free_rl_amd import Context
+    c = Context(device=0)
+    yield c
+    c.close()
+
+
+def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
+    from oracle import pyoracle as po
+    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    pol = po.perbin_model(2 * D, list(widths), head)
+    val = po.full_model(B * 2 * D, [64, 32], 1)
+    return po.Trainer(po.OR_PPO if algo == "ppo" else po.OR_AC, B, D, N, T, pol,
+                      pp, val, vp, lr_pi=1e-4 if algo == "ppo" else 1e-5,
+                      lr_v=1e-5 if algo == "ppo" else 1e-4, x0=x0)
+
+
+@pytest.mark.parametrize("algo,B,D,widths,N,T", [
+    ("ppo", 64, 2, (128, 128), 32, 4),   # BASELINE config 3 shape
+    ("ppo", 32, 1, (64, 64), 64, 4),     # config 2 shape
+    ("ac", 16, 2, (64, 64), 64, 8),
+])
+def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_ADV, BUF_BINS,
+                                                BUF_DONE, BUF_POLD,
+                                                BUF_POLICY_GRADS, BUF_VALUE_GRAD)
+    x0 = 987654321
+    pp = init_policy(D, *widths, seed=3)
+    vp = init_value(B, D, seed=4)
+    tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
+                 widths=widths, rng_state=x0)
+    tr.set_params(POLICY, pp)
+    tr.set_params(VALUE, vp)
+    orc = _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo)
+    for it in range(2):
+        tr.rollout()
+        acts = tr.buffer(BUF_ACTION)            # [T][N]
+        orc.rollout()                           # free-running oracle sampler
+        o_choice = orc.buf(po.BUF_STEP_CHOICE).reshape(N, T).T
+        np.testing.assert_array_equal(acts, o_choice)
+        bins = tr.buffer(BUF_BINS)
+        np.testing.assert_array_equal(
+            bins[:T], orc.buf(po.BUF_STEP_BINS).reshape(N, T, B, D).swapaxes(0, 1))
+        np.testing.assert_array_equal(
+            bins[T], orc.buf(po.BUF_FINAL_BINS).reshape(N, B, D))
+        np.testing.assert_array_equal(
+            tr.buffer(BUF_DONE), orc.buf(po.BUF_STEP_DONE).reshape(N, T).T)
+        assert_close(tr.buffer(BUF_POLD),
+                     orc.buf(po.BUF_STEP_PCHOICE).reshape(N, T).T, what="p_old")
+        tr.learn()
+        orc.learn()
+        # advantages of transition rows, in (t, env) order
+        env = orc.buf(po.BUF_ROW_ENV)
+        step = orc.buf(po.BUF_ROW_STEP) - it * T
+        is_end = orc.buf(po.BUF_ROW_IS_END)
+        oadv = orc.buf(po.BUF_ADVANTAGES)
+        adv = tr.buffer(BUF_ADV)
+        m = is_end == 0
+        assert_close(adv[step[m], env[m]], oadv[m], what="advantages")
+        assert_close(tr.buffer(BUF_VALUE_GRAD), orc.buf(po.BUF_VALUE_GRAD),
+                     what="value_grad")
+        assert_close(tr.params(VALUE), orc.params(1), what="value params")
+        assert_close(tr.buffer(BUF_POLICY_GRADS).ravel(),
+                     orc.buf(po.BUF_POLICY_GRADS), tol=3e-4, what="policy_grads")
+        assert_close(tr.params(POLICY), orc.params(0), what="policy params")
+
+
+def test_c3_full_size_properties(ctx):
+    """BASELINE config 3 (32768 envs x 64 bins x 2-D, [128,128], T=4): env
+    transition invariants on every env, probability normalisation, finite
+    learner state, and bitwise run-to-run determinism."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_ADV, BUF_BINS,
+                                                BUF_DONE, BUF_ITEMS, BUF_POLD,
+                                                BUF_PROBS)
+    N, B, D, T = 32768, 64, 2, 4
+    pp, vp = init_policy(D, 128, 128, seed=1), init_value(B, D, seed=2)
+
+    def make():
+        tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
+                     rng_state=20241008)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        return tr
+
+    tr = make()
+    tr.iterate(2)
+    tr.rollout()
+    bins = tr.buffer(BUF_BINS).astype(np.int32)
+    items = tr.buffer(BUF_ITEMS)[:, :, :D].astype(np.int32)
+    act = tr.buffer(BUF_ACTION)
+    done = tr.buffer(BUF_DONE)
+    assert bins.min() >= 0 and bins.max() <= 8  # stored states never negative
+    assert act.min() >= 0 and act.max() < B
+    ok_items = ((items == [4, 2]).all(-1) | (items == [1, 2]).all(-1))
+    assert ok_items.all()
+    for t in range(T):
+        nxt = bins[t].copy()
+        idx = np.arange(N)
+        nxt[idx, act[t]] -= items[t]
+        over = (nxt[idx, act[t]] < 0).any(-1)
+        np.testing.assert_array_equal(over.astype(np.uint8), done[t])
+        keep = ~over
+        np.testing.assert_array_equal(bins[t + 1][keep], nxt[keep])
+        assert (bins[t + 1][over] == 8).all()
+    probs = tr.buffer(BUF_PROBS)
+    np.testing.assert_allclose(probs.sum(1), 1.0, atol=1e-5)
+    pold = tr.buffer(BUF_POLD)
+    assert (pold > 0).all() and (pold <= 1).all()
+    tr.learn()
+    p1 = tr.params(POLICY)
+    assert np.isfinite(p1).all() and np.isfinite(tr.params(VALUE)).all()
+    assert np.isfinite(tr.buffer(BUF_ADV)).all()
+    # determinism: same seed, same params -> bitwise identical result
+    tr2 = make()
+    tr2.iterate(3)
+    np.testing.assert_array_equal(tr2.params(POLICY), p1)
