@@ -81,6 +81,23 @@ def cpu_baseline(seconds_budget=20.0):
                 n_env, T, iters)}
 
 
+def pmc_traffic(kernel="policy_train_kernel"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE summary (separate --pmc passes; see
+    tools/pmc_summary.py).  Raw counters (FETCH_SIZE is not x2-corrected: the
+    kernel's reads are narrow int8 loads, for which the gfx950 x2 correction
+    of wide streaming reads does not apply)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f).get(kernel)
+    if not s:
+        return None, None
+    return s["hbm_bytes"], os.path.relpath(files[-1], REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +161,10 @@ def main():
     # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
     avg_ms = ms_pt / max(n_pt, 1)
+    traffic, traffic_src = pmc_traffic()
+    # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
+    # p_old, advantage (12 B); per workgroup one f32 gradient slab
+    alg_bytes = n * T * (B * D + 4 + 12) + 256 * 17344 * 4
     achieved = flops_epoch / (avg_ms * 1e-3) / 1e12
     line = {
         "metric": "env-steps/sec (whole node) PPO bin-packing 64-bin",
@@ -169,7 +190,9 @@ def main():
                      "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s",
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                     "traffic": None,
+                     "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
                      "flops_per_launch": flops_epoch},
         "phase_ms_per_step": {

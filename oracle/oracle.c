@@ -736,6 +736,8 @@ void or_trainer_learn(or_trainer *t) {
   buf_set(&t->buf[OR_BUF_ROW_ENV], renv, rows, sizeof(int32_t));
   buf_set(&t->buf[OR_BUF_ROW_STEP], rstep, rows, sizeof(int32_t));
   buf_set(&t->buf[OR_BUF_ROW_IS_END], rend, rows, sizeof(int32_t));
+  buf_set(&t->buf[OR_BUF_ROW_CHOICE], choice, rows, sizeof(int32_t));
+  buf_set(&t->buf[OR_BUF_ROW_POLD], pold, rows, sizeof(float));
   buf_clear(&t->buf[OR_BUF_POLICY_GRADS]);
 
   float *adv = (float *)calloc(rows, sizeof(float));
@@ -869,6 +871,23 @@ void or_trainer_learn(or_trainer *t) {
     t->list[w++] = tj;
   }
   t->nlist = w;
+}
+
+void or_policy_grad_rows(const or_model *m, const float *params, const float *x,
+                         int rows, int xcols, const int32_t *choice,
+                         const float *pold, const float *adv, int algo,
+                         float *grad) {
+  int *ch = (int *)malloc(sizeof(int) * (rows > 0 ? rows : 1));
+  for (int r = 0; r < rows; ++r) ch[r] = choice[r];
+  pl_ctx pc = {ch, pold, adv, algo == OR_PPO};
+  or_model_grad(m, params, x, rows, xcols, loss_policy, &pc, grad);
+  free(ch);
+}
+
+void or_value_grad_rows(const or_model *m, const float *params, const float *x,
+                        int rows, int xcols, const float *targets, float *grad) {
+  sq_ctx sc = {targets};
+  or_model_grad(m, params, x, rows, xcols, loss_square, &sc, grad);
 }
 
 /* deep_agent.cc:25-41 / policy_gradient_deterministic_policy

@@ -117,10 +117,22 @@ enum {
   OR_BUF_POLICY_GRADS,  /* float  [epochs][policy params]                  */
   OR_BUF_FINAL_BINS,    /* int32  [N][B][D]  env states after the rollout   */
   OR_BUF_FINAL_ITEM,    /* int32  [N][D]                                   */
+  OR_BUF_ROW_CHOICE,    /* int32  [rows]  action of the row                */
+  OR_BUF_ROW_POLD,      /* float  [rows]  distrib[choice] of the row       */
   OR_BUF_COUNT
 };
 /* Returns a pointer to the buffer and its element count. */
 const void *or_trainer_buf(const or_trainer *t, int which, size_t *count);
+
+/* Gradient of one loss over an explicit set of rows (any subset of a learn()
+ * batch): the building block of the sharded (multi-rank) check.  algo selects
+ * the loss as in or_trainer_learn (PPO surrogate / AC and PG softmax-log). */
+void or_policy_grad_rows(const or_model *m, const float *params, const float *x,
+                         int rows, int xcols, const int32_t *choice,
+                         const float *pold, const float *adv, int algo,
+                         float *grad);
+void or_value_grad_rows(const or_model *m, const float *params, const float *x,
+                        int rows, int xcols, const float *targets, float *grad);
 
 /* Deterministic (argmax) evaluation, deep_agent.cc:25-41: `episodes` episodes
  * on one env seeded at x0; returns total reward, engine state via *x. */

@@ -17,10 +17,10 @@ OR_PPO, OR_AC, OR_PG = range(3)
 (BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE, BUF_STEP_PCHOICE,
  BUF_ROWS, BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_VALUES, BUF_TARGETS,
  BUF_VALUE_GRAD, BUF_ADVANTAGES, BUF_POLICY_GRADS, BUF_FINAL_BINS,
- BUF_FINAL_ITEM) = range(16)
+ BUF_FINAL_ITEM, BUF_ROW_CHOICE, BUF_ROW_POLD) = range(18)
 _INT_BUFS = {BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE,
              BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_FINAL_BINS,
-             BUF_FINAL_ITEM}
+             BUF_FINAL_ITEM, BUF_ROW_CHOICE}
 
 
 class EnvCfg(C.Structure):
@@ -79,6 +79,11 @@ def lib():
         l.or_trainer_set_params.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         l.or_trainer_buf.restype = C.c_void_p
         l.or_trainer_buf.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]
+        l.or_policy_grad_rows.argtypes = [C.POINTER(Model), C.c_void_p, C.c_void_p,
+                                          C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_int, C.c_void_p]
+        l.or_value_grad_rows.argtypes = [C.POINTER(Model), C.c_void_p, C.c_void_p,
+                                         C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         l.or_eval_argmax.restype = C.c_double
         l.or_eval_argmax.argtypes = [C.POINTER(EnvCfg), C.POINTER(Model),
                                      C.c_void_p, C.c_long, u32p]
@@ -254,6 +259,29 @@ class Trainer:
             return np.zeros(0, dt)
         arr = (C.c_int32 if dt == np.int32 else C.c_float) * n.value
         return np.frombuffer(arr.from_address(p), dt).copy()
+
+
+def policy_grad_rows(model, params, x, choice, pold, adv, algo):
+    x = np.ascontiguousarray(x, np.float32)
+    params = np.ascontiguousarray(params, np.float32)
+    ch = np.ascontiguousarray(choice, np.int32)
+    pold = np.ascontiguousarray(pold, np.float32)
+    adv = np.ascontiguousarray(adv, np.float32)
+    g = np.zeros(nparams(model), np.float32)
+    lib().or_policy_grad_rows(C.byref(model), _ptr(params), _ptr(x), x.shape[0],
+                              x.shape[1], _ptr(ch), _ptr(pold), _ptr(adv), algo,
+                              _ptr(g))
+    return g
+
+
+def value_grad_rows(model, params, x, targets):
+    x = np.ascontiguousarray(x, np.float32)
+    params = np.ascontiguousarray(params, np.float32)
+    tg = np.ascontiguousarray(targets, np.float32)
+    g = np.zeros(nparams(model), np.float32)
+    lib().or_value_grad_rows(C.byref(model), _ptr(params), _ptr(x), x.shape[0],
+                             x.shape[1], _ptr(tg), _ptr(g))
+    return g
 
 
 def eval_argmax(B, D, model, params, episodes, x0):
