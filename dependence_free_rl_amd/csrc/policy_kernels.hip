@@ -81,49 +81,64 @@ __device__ __forceinline__ void stage_params(const float *__restrict__ P,
   if (tid == 0) lds[S::L_B3] = P[L.ob3()];
 }
 
-// Observation feature f of bin `bin` in env `env` at trajectory slot `slot`
-// (observation::to_vector, bin_packing.h:31-40): [bin dims / 8, item dims / 8].
+// The raw int8 state of the two rows a lane carries (rows rt*32 + lane&31 of
+// a group), fetched one group ahead so the global-load latency overlaps the
+// previous group's MFMA work (1 wave per SIMD in the train kernel).
 template <class S>
-__device__ __forceinline__ void load_row(const Batch &b, int slot, int env,
-                                         int bin, int (&bv)[S::D],
-                                         int (&iv)[S::D]) {
-  const int8_t *bp = b.bins + ((size_t)slot * b.N + env) * S::BD + bin * S::D;
-  const int8_t *ip = b.items + ((size_t)slot * b.N + env) * 4;
+struct RowRaw {
+  int bv[2][S::D];
+  int iv[2][S::D];
+};
+
+template <class S>
+__device__ __forceinline__ void fetch_rows(const Batch &b, int slot, int e0,
+                                           RowRaw<S> &rr) {
+  const int lr = threadIdx.x & 31;
 #pragma unroll
-  for (int d = 0; d < S::D; ++d) {
-    bv[d] = bp[d];
-    iv[d] = ip[d];
+  for (int rt = 0; rt < 2; ++rt) {
+    const int r = rt * 32 + lr;
+    const size_t env = (size_t)slot * b.N + e0 + r / S::B;
+    const int8_t *bp = b.bins + env * S::BD + (r % S::B) * S::D;
+    const int8_t *ip = b.items + env * 4;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      rr.bv[rt][d] = bp[d];
+      rr.iv[rt][d] = ip[d];
+    }
   }
 }
 
+// Observation feature f of a row (observation::to_vector, bin_packing.h:31-40):
+// [bin dims / 8, item dims / 8].  f may be runtime (lane-half dependent).
 template <class S>
-__device__ __forceinline__ float feature(const int (&bv)[S::D],
-                                         const int (&iv)[S::D], int f) {
+__device__ __forceinline__ float row_feature(const RowRaw<S> &rr, int rt,
+                                             int f) {
   int v = 0;
 #pragma unroll
   for (int d = 0; d < S::D; ++d) {
-    if (f == d) v = bv[d];
-    if (f == S::D + d) v = iv[d];
+    if (f == d) v = rr.bv[rt][d];
+    if (f == S::D + d) v = rr.iv[rt][d];
   }
   return f < S::F0 ? (float)v / (float)kCapacity : 0.0f;
+}
+
+// 4 consecutive LDS floats (16-byte aligned) -> bias / weight values of
+// accumulator registers 4q..4q+3 (acc_row = 8q + 4h + {0..3}).
+__device__ __forceinline__ float4 lds4(const float *p) {
+  return *reinterpret_cast<const float4 *>(p);
 }
 
 // Layer 1 (F0 -> H1) + bias + relu for the 64 rows of a group, all H1 tiles.
 // h1[it][rt]: col = row rt*32 + (lane&31), acc row = feature it*32+acc_row.
 template <class S>
-__device__ __forceinline__ void layer1(const Batch &b, int slot, int e0,
-                                       const float *lds,
+__device__ __forceinline__ void layer1(const RowRaw<S> &rr, const float *lds,
                                        f32x16 (&h1)[S::NIT][2]) {
   const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
   float xb[2][S::S1];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    const int r = rt * 32 + lr;
-    int bv[S::D], iv[S::D];
-    load_row<S>(b, slot, e0 + r / S::B, r % S::B, bv, iv);
+  for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int s = 0; s < S::S1; ++s) xb[rt][s] = feature<S>(bv, iv, 2 * s + h);
-  }
+    for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(rr, rt, 2 * s + h);
 #pragma unroll
   for (int it = 0; it < S::NIT; ++it) {
     float wa[S::S1];
@@ -132,46 +147,65 @@ __device__ __forceinline__ void layer1(const Batch &b, int slot, int e0,
       const int k = 2 * s + h;
       wa[s] = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
     }
+    f32x16 acc0 = zero16(), acc1 = zero16();
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      f32x16 acc = zero16();
-#pragma unroll
-      for (int s = 0; s < S::S1; ++s) acc = mfma32(wa[s], xb[rt][s], acc);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float v = acc[j] + lds[S::L_B1 + it * 32 + acc_row(j, h)];
-        acc[j] = v > 0.0f ? v : 0.0f;
-      }
-      h1[it][rt] = acc;
+    for (int s = 0; s < S::S1; ++s) {
+      acc0 = mfma32(wa[s], xb[0][s], acc0);
+      acc1 = mfma32(wa[s], xb[1][s], acc1);
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * q + 4 * h);
+      const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float v0 = acc0[4 * q + u] + bq[u];
+        const float v1 = acc1[4 * q + u] + bq[u];
+        acc0[4 * q + u] = v0 > 0.0f ? v0 : 0.0f;
+        acc1[4 * q + u] = v1 > 0.0f ? v1 : 0.0f;
+      }
+    }
+    h1[it][0] = acc0;
+    h1[it][1] = acc1;
   }
 }
 
-// Layer 2 pre-activation (+ bias) for output tile o2t and r-tile rt:
-// A = W2 rows from the LDS image (4 k-steps per ds_read_b128), B = h1 regs.
-template <class S>
-__device__ __forceinline__ f32x16 layer2(const float *lds,
-                                         const f32x16 (&h1)[S::NIT][2],
-                                         int o2t, int rt) {
+// Layer 2 pre-activations (+ bias) of output tile o2t for NR r-tiles
+// rt0..rt0+NR-1: A = W2 rows from the LDS image (4 k-steps per ds_read_b128,
+// shared by the NR independent accumulation chains), B = h1 registers.
+template <class S, int NR>
+__device__ __forceinline__ void layer2(const float *lds,
+                                       const f32x16 (&h1)[S::NIT][2], int o2t,
+                                       int rt0, f32x16 (&acc)[NR]) {
   const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
   const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
-  f32x16 acc = zero16();
+#pragma unroll
+  for (int r = 0; r < NR; ++r) acc[r] = zero16();
 #pragma unroll
   for (int it = 0; it < S::NIT; ++it) {
-    // select with a compile-time index (a runtime index would spill h1)
-    const f32x16 hb = rt == 0 ? h1[it][0] : h1[it][1];
+    f32x16 hb[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)  // compile-time index when NR == 2
+      hb[r] = NR == 2 ? h1[it][r] : (rt0 == 0 ? h1[it][0] : h1[it][1]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 a4 = *reinterpret_cast<const float4 *>(wrow + it * 32 + 8 * q);
-      acc = mfma32(a4.x, hb[4 * q + 0], acc);
-      acc = mfma32(a4.y, hb[4 * q + 1], acc);
-      acc = mfma32(a4.z, hb[4 * q + 2], acc);
-      acc = mfma32(a4.w, hb[4 * q + 3], acc);
+      const float4 a4 = lds4(wrow + it * 32 + 8 * q);
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] = mfma32(av[u], hb[r][4 * q + u], acc[r]);
     }
   }
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] += lds[S::L_B2 + o2t * 32 + acc_row(j, h)];
-  return acc;
+  for (int q = 0; q < 4; ++q) {
+    const float4 bb = lds4(lds + S::L_B2 + o2t * 32 + 8 * q + 4 * h);
+    const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[r][4 * q + u] += bq[u];
+  }
 }
 
 // Partial logit over this tile's 32 H2 units for row rt*32 + (lane&31).
@@ -181,9 +215,14 @@ __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
   const int h = (threadIdx.x & 63) >> 5;
   float zp = 0.0f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const float v = pre[j] > 0.0f ? pre[j] : 0.0f;
-    zp += v * lds[S::L_W3 + o2t * 32 + acc_row(j, h)];
+  for (int q = 0; q < 4; ++q) {
+    const float4 ww = lds4(lds + S::L_W3 + o2t * 32 + 8 * q + 4 * h);
+    const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = pre[4 * q + u] > 0.0f ? pre[4 * q + u] : 0.0f;
+      zp += v * wq[u];
+    }
   }
   return zp + __shfl_xor(zp, 32, kWave);
 }
@@ -194,7 +233,8 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
   const int N = a.b.N, t = a.t;
   const int ngroups = N / S::G;
   // forward job of this wave: output tile o2t, r-tiles rt0 .. rt0+FJ-1
@@ -202,18 +242,22 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
   const int rt0 = S::NOT >= 4 ? 0 : w / S::NOT;
   const bool fwd_active = (w / S::NOT) * S::FJ < 2;
 
+  RowRaw<S> cur, nxt;
+  if ((int)blockIdx.x < ngroups) fetch_rows<S>(a.b, t, blockIdx.x * S::G, cur);
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int e0 = g * S::G;
+    const int gn = g + gridDim.x;
+    if (gn < ngroups) fetch_rows<S>(a.b, t, gn * S::G, nxt);
     {
       f32x16 h1[S::NIT][2];
-      layer1<S>(a.b, t, e0, lds, h1);
+      layer1<S>(cur, lds, h1);
       if (fwd_active) {
+        f32x16 pre[S::FJ];
+        layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
 #pragma unroll
         for (int q = 0; q < S::FJ; ++q) {
-          const int rt = rt0 + q;
-          const f32x16 pre = layer2<S>(lds, h1, o2t, rt);
-          const float zp = logit_part<S>(lds, pre, o2t);
-          if (lane < 32) lds[S::L_Z + o2t * 64 + rt * 32 + lr] = zp;
+          const float zp = logit_part<S>(lds, pre[q], o2t);
+          if (lane < 32) lds[S::L_Z + o2t * 64 + (rt0 + q) * 32 + lr] = zp;
         }
       }
     }
@@ -268,13 +312,14 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
       }
       const float pold = wave_shfl(p, seg0 + choice);
 
-      int bv[S::D], iv[S::D];
-      load_row<S>(a.b, t, env, bin, bv, iv);
+      // this lane's row (= lane) is row (h ? 32 : 0) + lr of the prefetch
       int nb[S::D];
       int neg = 0;
 #pragma unroll
       for (int d = 0; d < S::D; ++d) {
-        nb[d] = bin == choice ? bv[d] - iv[d] : bv[d];
+        const int bv = h ? cur.bv[1][d] : cur.bv[0][d];
+        const int iv = h ? cur.iv[1][d] : cur.iv[0][d];
+        nb[d] = bin == choice ? bv - iv : bv;
         neg |= nb[d] < 0;
       }
       const int done = __shfl(neg, seg0 + choice, kWave);
@@ -295,6 +340,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
       }
     }
     __syncthreads();
+    cur = nxt;
   }
 }
 
@@ -318,7 +364,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
   const int rt0 = NOT >= 4 ? 0 : w / NOT;
   const bool fwd_active = (w / NOT) * S::FJ < 2;
   const int it_own = w % NIT;             // dH1 / dW1 tile
-  const int hrt0 = w / NIT;               // first dH1 r-tile
+  const int hrt0 = NIT >= 4 ? 0 : w / NIT;  // first dH1 r-tile
   constexpr int HSTEP = 4 / NIT;          // r-tile stride between slots
 
   // persistent accumulators
@@ -333,13 +379,28 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
     for (int f = 0; f < S::F0; ++f) accW1[j][f] = 0.0f;
   }
 
-  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  // prefetched per-group inputs: two rows per lane + this lane's env record
+  RowRaw<S> cur, nxt;
+  int c_cur = 0, c_nxt = 0;
+  float po_cur = 1.0f, po_nxt = 1.0f, A_cur = 0.0f, A_nxt = 0.0f;
+  auto fetch = [&](int g, RowRaw<S> &rr, int &c, float &po, float &A) {
     const int t = g / gpt, e0 = (g - t * gpt) * S::G;
+    fetch_rows<S>(a.b, t, e0, rr);
+    const size_t ti = (size_t)t * N + e0 + lane / B;
+    c = a.b.action[ti];
+    po = a.b.pold[ti];
+    A = a.adv[ti];
+  };
+  if ((int)blockIdx.x < ngroups) fetch(blockIdx.x, cur, c_cur, po_cur, A_cur);
+
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int gn = g + gridDim.x;
+    if (gn < ngroups) fetch(gn, nxt, c_nxt, po_nxt, A_nxt);
     f32x16 pre[S::FJ];
     f32x16 h1own[2];
     {
       f32x16 h1[NIT][2];
-      layer1<S>(a.b, t, e0, lds, h1);
+      layer1<S>(cur, lds, h1);
       // H1 image for dW2 (each H1 tile written by one wave)
       if (w < NIT) {
 #pragma unroll
@@ -360,12 +421,11 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
           h1own[1] = h1[it][1];
         }
       if (fwd_active) {
+        layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
 #pragma unroll
         for (int q = 0; q < S::FJ; ++q) {
-          const int rt = rt0 + q;
-          pre[q] = layer2<S>(lds, h1, o2t, rt);
           const float zp = logit_part<S>(lds, pre[q], o2t);
-          if (lane < 32) lds[S::L_Z + o2t * 64 + rt * 32 + lr] = zp;
+          if (lane < 32) lds[S::L_Z + o2t * 64 + (rt0 + q) * 32 + lr] = zp;
         }
       }
     }
@@ -374,21 +434,20 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
     // ---- logits -> softmax -> loss gradient w.r.t. logits (lane = row)
     float gz;
     {
-      const int e = lane / B, bin = lane % B, env = e0 + e, seg0 = e * B;
+      const int bin = lane % B, seg0 = (lane / B) * B;
       float zs = 0.0f;
 #pragma unroll
       for (int o = 0; o < NOT; ++o) zs += lds[S::L_Z + o * 64 + lane];
       const float z = zs + lds[S::L_B3];
       const float ex = expf(z);
       const float p = ex / seg_sum<B>(ex);
-      const size_t ti = (size_t)t * N + env;
-      const int c = a.b.action[ti];
-      const float A = a.adv[ti];
+      const int c = c_cur;
+      const float A = A_cur;
       if (a.algo == kPPO) {
         // clipped_gradient (rl.h:54-74) then softmax_layer::backward
         // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
         const float pc = wave_shfl(p, seg0 + c);
-        const float ratio = pc / a.b.pold[ti];
+        const float ratio = pc / po_cur;
         float clipped = ratio;
         if (ratio > 1.0f + a.clip_eps)
           clipped = 1.0f + a.clip_eps;
@@ -413,64 +472,78 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
         const int rt = rt0 + q;
         const float gr = wave_shfl(gz, rt * 32 + lr);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int o2 = o2t * 32 + acc_row(j, h);
-          const float v = pre[q][j];
-          const float h2 = v > 0.0f ? v : 0.0f;
-          accW3[j] += gr * h2;
-          const float d = v > 0.0f ? gr * lds[S::L_W3 + o2] : 0.0f;
-          accB2[j] += d;
-          DAimg[(rt * 32 + lr) * S::AS + o2] = d;
+        for (int qq = 0; qq < 4; ++qq) {
+          const float4 ww = lds4(lds + S::L_W3 + o2t * 32 + 8 * qq + 4 * h);
+          const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = 4 * qq + u;
+            const float v = pre[q][j];
+            const float h2 = v > 0.0f ? v : 0.0f;
+            accW3[j] += gr * h2;
+            const float d = v > 0.0f ? gr * wq[u] : 0.0f;
+            accB2[j] += d;
+            DAimg[(rt * 32 + lr) * S::AS + o2t * 32 + acc_row(j, h)] = d;
+          }
         }
       }
     }
     __syncthreads();
 
-    // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows)
+    // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows); the JW
+    // independent accumulation chains share the dA2 operand
+#pragma unroll 4
+    for (int s = 0; s < 32; ++s) {
+      const int r = 2 * s + h;
+      const float av = DAimg[r * S::AS + o2t * 32 + lr];
 #pragma unroll
-    for (int q = 0; q < S::JW; ++q) {
-      const int it = w / NOT + q * (4 / NOT);
-      if (it < NIT) {
-        f32x16 acc = accW2[q];
-#pragma unroll 8
-        for (int s = 0; s < 32; ++s) {
-          const int r = 2 * s + h;
-          acc = mfma32(DAimg[r * S::AS + o2t * 32 + lr],
-                       H1img[r * S::HS + it * 32 + lr], acc);
-        }
-        accW2[q] = acc;
+      for (int q = 0; q < S::JW; ++q) {
+        const int it = NOT >= 4 ? q : w / NOT + q * (4 / NOT);
+        if (NOT >= 4 || it < NIT)
+          accW2[q] = mfma32(av, H1img[r * S::HS + it * 32 + lr], accW2[q]);
       }
     }
 
     // ---- dH1^T[i][r] = sum_o2 W2[o2][i] dA2[r][o2]; relu'; dW1, db1
+    {
+      f32x16 dh[S::JH];
 #pragma unroll
-    for (int q = 0; q < S::JH; ++q) {
-      const int rt = hrt0 + q * HSTEP;
-      if (rt < 2) {
-        f32x16 acc = zero16();
-#pragma unroll 8
-        for (int s = 0; s < S::H2 / 2; ++s) {
-          const int k = 2 * s + h;
-          acc = mfma32(lds[S::L_W2 + k * S::W2S + it_own * 32 + lr],
-                       DAimg[(rt * 32 + lr) * S::AS + k], acc);
+      for (int q = 0; q < S::JH; ++q) dh[q] = zero16();
+#pragma unroll 4
+      for (int s = 0; s < S::H2 / 2; ++s) {
+        const int k = 2 * s + h;
+        const float av = lds[S::L_W2 + k * S::W2S + it_own * 32 + lr];
+#pragma unroll
+        for (int q = 0; q < S::JH; ++q) {
+          const int rt = NIT >= 4 ? q : hrt0 + q * HSTEP;
+          if (NIT >= 4 || rt < 2)
+            dh[q] = mfma32(av, DAimg[(rt * 32 + lr) * S::AS + k], dh[q]);
         }
-        const int r = rt * 32 + lr;
-        int bv[S::D], iv[S::D];
-        load_row<S>(a.b, t, e0 + r / B, r % B, bv, iv);
-        float xf[S::F0];
+      }
 #pragma unroll
-        for (int f = 0; f < S::F0; ++f) xf[f] = feature<S>(bv, iv, f);
-        const f32x16 hv = (rt == 0) ? h1own[0] : h1own[1];
+      for (int q = 0; q < S::JH; ++q) {
+        const int rt = NIT >= 4 ? q : hrt0 + q * HSTEP;
+        if (NIT >= 4 || rt < 2) {
+          float xf[S::F0];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float d = hv[j] > 0.0f ? acc[j] : 0.0f;
-          accB1[j] += d;
+          for (int f = 0; f < S::F0; ++f)
+            xf[f] = rt == 0 ? row_feature<S>(cur, 0, f) : row_feature<S>(cur, 1, f);
+          const f32x16 hv = (rt == 0) ? h1own[0] : h1own[1];
 #pragma unroll
-          for (int f = 0; f < S::F0; ++f) accW1[j][f] += d * xf[f];
+          for (int j = 0; j < 16; ++j) {
+            const float d = hv[j] > 0.0f ? dh[q][j] : 0.0f;
+            accB1[j] += d;
+#pragma unroll
+            for (int f = 0; f < S::F0; ++f) accW1[j][f] += d * xf[f];
+          }
         }
       }
     }
     __syncthreads();
+    cur = nxt;
+    c_cur = c_nxt;
+    po_cur = po_nxt;
+    A_cur = A_nxt;
   }
 
   // ---------------------------------------------------- slab write-out ----
