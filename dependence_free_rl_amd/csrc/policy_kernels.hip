@@ -421,7 +421,12 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
           h1own[1] = h1[it][1];
         }
       if (fwd_active) {
-        layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
+        if (!(a.ablate & 4)) {
+          layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
+        } else {
+#pragma unroll
+          for (int q = 0; q < S::FJ; ++q) pre[q] = h1[0][q & 1];
+        }
 #pragma unroll
         for (int q = 0; q < S::FJ; ++q) {
           const float zp = logit_part<S>(lds, pre[q], o2t);
@@ -443,7 +448,9 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
       const float p = ex / seg_sum<B>(ex);
       const int c = c_cur;
       const float A = A_cur;
-      if (a.algo == kPPO) {
+      if (a.ablate & 8) {
+        gz = z * 1e-3f;
+      } else if (a.algo == kPPO) {
         // clipped_gradient (rl.h:54-74) then softmax_layer::backward
         // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
         const float pc = wave_shfl(p, seg0 + c);
@@ -493,7 +500,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
     // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows); the JW
     // independent accumulation chains share the dA2 operand
 #pragma unroll 4
-    for (int s = 0; s < 32; ++s) {
+    for (int s = 0; s < ((a.ablate & 1) ? 0 : 32); ++s) {
       const int r = 2 * s + h;
       const float av = DAimg[r * S::AS + o2t * 32 + lr];
 #pragma unroll
@@ -510,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
 #pragma unroll
       for (int q = 0; q < S::JH; ++q) dh[q] = zero16();
 #pragma unroll 4
-      for (int s = 0; s < S::H2 / 2; ++s) {
+      for (int s = 0; s < ((a.ablate & 2) ? 0 : S::H2 / 2); ++s) {
         const int k = 2 * s + h;
         const float av = lds[S::L_W2 + k * S::W2S + it_own * 32 + lr];
 #pragma unroll
@@ -621,6 +628,289 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
   }
 }
 
+// ================================================ train epoch, 8 waves ====
+// H1 = H2 = 128 (BASELINE configs 3/4/5): 512-thread workgroup = 2 waves per
+// SIMD so one wave's LDS / VALU / barrier time hides behind its partner's
+// MFMAs.  Wave w = (q = w&3, rt = w>>2) owns:
+//   forward    H2 tile q of r-tile rt (layer 1 fused tile by tile into the
+//              layer-2 k-loop, so only one 16-register H1 tile is live)
+//   dW2        tiles (q, 2rt) and (q, 2rt+1), K = all 64 rows
+//   dH1 / dW1  H1 tile q of r-tile rt
+template <class S>
+__global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a) {
+  static_assert(S::NIT == 4 && S::NOT == 4, "8-wave kernel is for 128x128");
+  static_assert(8 * S::RED <= 64 * S::HS + 64 * S::AS, "scratch fits");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  constexpr int B = S::B;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int q = w & 3, rt = w >> 2;
+  const int N = a.b.N, T = a.b.T;
+  const int gpt = N / S::G;
+  const int ngroups = T * gpt;
+  float *H1img = lds + S::L_H1;
+  float *DAimg = lds + S::L_DA2;
+
+  f32x16 accW2[2];
+  accW2[0] = zero16();
+  accW2[1] = zero16();
+  float accW1[16][S::F0], accB1[16], accW3[16], accB2[16], accB3 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    accB1[j] = accW3[j] = accB2[j] = 0.0f;
+#pragma unroll
+    for (int f = 0; f < S::F0; ++f) accW1[j][f] = 0.0f;
+  }
+
+  // this lane's row (rt*32 + lr) of the next group is fetched one group
+  // ahead; its env record (action, p_old, advantage) at the start of the
+  // group it is used in (consumed after the forward pass).
+  int bv_c[S::D], iv_c[S::D], bv_n[S::D], iv_n[S::D];
+  auto fetch_row = [&](int g, int (&bv)[S::D], int (&iv)[S::D]) {
+    const int t = g / gpt, e0 = (g - t * gpt) * S::G;
+    const int r = rt * 32 + lr;
+    const size_t env = (size_t)t * N + e0 + r / B;
+    const int8_t *bp = a.b.bins + env * S::BD + (r % B) * S::D;
+    const int8_t *ip = a.b.items + env * 4;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      bv[d] = bp[d];
+      iv[d] = ip[d];
+    }
+  };
+  auto feat = [&](int f) {  // feature f of this lane's row (current group)
+    int v = 0;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      if (f == d) v = bv_c[d];
+      if (f == S::D + d) v = iv_c[d];
+    }
+    return f < S::F0 ? (float)v / (float)kCapacity : 0.0f;
+  };
+  if ((int)blockIdx.x < ngroups) fetch_row(blockIdx.x, bv_c, iv_c);
+
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int gn = g + gridDim.x;
+    if (gn < ngroups) fetch_row(gn, bv_n, iv_n);
+    int c_cur;
+    float po_cur, A_cur;
+    {
+      const int t = g / gpt, e0 = (g - t * gpt) * S::G;
+      const size_t ti = (size_t)t * N + e0 + lane / B;
+      c_cur = a.b.action[ti];
+      po_cur = a.b.pold[ti];
+      A_cur = a.adv[ti];
+    }
+
+    // ---- layer 1 tile by tile, fused into the layer-2 k-loop
+    f32x16 pre = zero16();
+    {
+      float xb[S::S1];
+#pragma unroll
+      for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
+      const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        f32x16 t1 = zero16();
+#pragma unroll
+        for (int s = 0; s < S::S1; ++s) {
+          const int k = 2 * s + h;
+          const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+          t1 = mfma32(wa, xb[s], t1);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
+          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float v = t1[4 * qq + u] + bq[u];
+            t1[4 * qq + u] = v > 0.0f ? v : 0.0f;
+          }
+        }
+        if (it == q) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            H1img[(rt * 32 + lr) * S::HS + it * 32 + acc_row(j, h)] = t1[j];
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
+          pre = mfma32(a4.x, t1[4 * qq + 0], pre);
+          pre = mfma32(a4.y, t1[4 * qq + 1], pre);
+          pre = mfma32(a4.z, t1[4 * qq + 2], pre);
+          pre = mfma32(a4.w, t1[4 * qq + 3], pre);
+        }
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
+        pre[4 * qq + 0] += bb.x;
+        pre[4 * qq + 1] += bb.y;
+        pre[4 * qq + 2] += bb.z;
+        pre[4 * qq + 3] += bb.w;
+      }
+      const float zp = logit_part<S>(lds, pre, q);
+      if (lane < 32) lds[S::L_Z + q * 64 + rt * 32 + lr] = zp;
+    }
+    __syncthreads();
+
+    // ---- logits -> softmax -> loss gradient w.r.t. logits (lane = row)
+    float gz;
+    {
+      const int bin = lane % B, seg0 = (lane / B) * B;
+      const float zs = ((lds[S::L_Z + lane] + lds[S::L_Z + 64 + lane]) +
+                        lds[S::L_Z + 128 + lane]) + lds[S::L_Z + 192 + lane];
+      const float z = zs + lds[S::L_B3];
+      const float ex = expf(z);
+      const float p = ex / seg_sum<B>(ex);
+      const int c = c_cur;
+      const float A = A_cur;
+      if (a.algo == kPPO) {
+        const float pc = wave_shfl(p, seg0 + c);
+        const float ratio = pc / po_cur;
+        float clipped = ratio;
+        if (ratio > 1.0f + a.clip_eps)
+          clipped = 1.0f + a.clip_eps;
+        else if (ratio < 1.0f - a.clip_eps)
+          clipped = 1.0f - a.clip_eps;
+        const float ig = fminf(clipped * A, ratio * A) * -1.0f;
+        const float gc = ig / pc;
+        const float lin = bin == c ? p : 0.0f;
+        gz = (lin - p * pc) * gc;
+      } else {
+        gz = p * A;
+        if (bin == c) gz -= A;
+      }
+      if (w == 0) accB3 += gz;
+    }
+
+    // ---- backward through layer 3 and the layer-2 relu (tile q, r-tile rt)
+    {
+      const float gr = wave_shfl(gz, rt * 32 + lr);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
+        const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = 4 * qq + u;
+          const float v = pre[j];
+          accW3[j] += gr * (v > 0.0f ? v : 0.0f);
+          const float d = v > 0.0f ? gr * wq[u] : 0.0f;
+          accB2[j] += d;
+          DAimg[(rt * 32 + lr) * S::AS + q * 32 + acc_row(j, h)] = d;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- dW2 tiles (q, 2rt), (q, 2rt+1): K = 64 rows
+#pragma unroll 4
+    for (int s = 0; s < 32; ++s) {
+      const int r = 2 * s + h;
+      const float av = DAimg[r * S::AS + q * 32 + lr];
+      accW2[0] = mfma32(av, H1img[r * S::HS + (2 * rt) * 32 + lr], accW2[0]);
+      accW2[1] = mfma32(av, H1img[r * S::HS + (2 * rt + 1) * 32 + lr], accW2[1]);
+    }
+
+    // ---- dH1 tile q of r-tile rt (K = H2); relu'; dW1, db1
+    {
+      f32x16 dh = zero16();
+#pragma unroll 8
+      for (int s = 0; s < S::H2 / 2; ++s) {
+        const int k = 2 * s + h;
+        dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
+                    DAimg[(rt * 32 + lr) * S::AS + k], dh);
+      }
+      float xf[S::F0];
+#pragma unroll
+      for (int f = 0; f < S::F0; ++f) xf[f] = feat(f);
+      const float *hrow = H1img + (rt * 32 + lr) * S::HS + q * 32;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        // relu' from the H1 image this wave wrote (post-relu > 0 <=> pre > 0)
+        const float d = hrow[acc_row(j, h)] > 0.0f ? dh[j] : 0.0f;
+        accB1[j] += d;
+#pragma unroll
+        for (int f = 0; f < S::F0; ++f) accW1[j][f] += d * xf[f];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      bv_c[d] = bv_n[d];
+      iv_c[d] = iv_n[d];
+    }
+  }
+
+  // ---------------------------------------------------- slab write-out ----
+  const PolicyLayout L{S::F0, S::H1, S::H2};
+  float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = 2 * rt + k;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int o2 = q * 32 + acc_row(j, h);
+      slab[L.oW2() + o2 * S::H1 + it * 32 + lr] = accW2[k][j];
+    }
+  }
+  float *scr = lds + S::L_H1;  // [8][RED] wave partials (aliases the images)
+  for (int i = threadIdx.x; i < 8 * S::RED; i += blockDim.x) scr[i] = 0.0f;
+  __syncthreads();
+  float *my = scr + w * S::RED;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    float vb1 = accB1[j], vw3 = accW3[j], vb2 = accB2[j];
+    float vw1[S::F0];
+#pragma unroll
+    for (int f = 0; f < S::F0; ++f) vw1[f] = accW1[j][f];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      vb1 += __shfl_xor(vb1, o, kWave);
+      vw3 += __shfl_xor(vw3, o, kWave);
+      vb2 += __shfl_xor(vb2, o, kWave);
+#pragma unroll
+      for (int f = 0; f < S::F0; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
+    }
+    if (lr == 0) {
+      const int i = q * 32 + acc_row(j, h);
+#pragma unroll
+      for (int f = 0; f < S::F0; ++f) my[i * S::F0 + f] = vw1[f];
+      my[S::H1 * S::F0 + i] = vb1;
+      my[S::H1 * S::F0 + S::H1 + i] = vw3;  // o2 = q*32 + acc_row too
+      my[S::H1 * S::F0 + S::H1 + S::H2 + i] = vb2;
+    }
+  }
+  {
+    float v = accB3;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+    if (lane == 0) my[S::RED - 1] = w == 0 ? v : 0.0f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < S::RED; i += blockDim.x) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += scr[k * S::RED + i];
+    int dst;
+    if (i < S::H1 * S::F0)
+      dst = L.oW1() + i;
+    else if (i < S::H1 * S::F0 + S::H1)
+      dst = L.ob1() + (i - S::H1 * S::F0);
+    else if (i < S::H1 * S::F0 + S::H1 + S::H2)
+      dst = L.ow3() + (i - S::H1 * S::F0 - S::H1);
+    else if (i < S::RED - 1)
+      dst = L.ob2() + (i - S::H1 * S::F0 - S::H1 - S::H2);
+    else
+      dst = L.ob3();
+    slab[dst] = v;
+  }
+}
+
 // ================================================================ dispatch ==
 #define XH_POLICY_SHAPES(X) \
   X(8, 2, 128, 64)          \
@@ -628,6 +918,10 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
   X(16, 2, 64, 64)          \
   X(32, 1, 64, 64)          \
   X(64, 2, 128, 128)
+
+#ifndef XH_TRAIN4
+#define XH_TRAIN4 0  // 1: force the 4-wave train kernel everywhere (A/B)
+#endif
 
 template <class S>
 constexpr size_t rollout_lds() {
@@ -702,10 +996,18 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
       (void)hipFuncSetAttribute((const void *)policy_train_kernel<S>,        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                 (int)train_lds<S>());                        \
+      if constexpr (S::NIT == 4 && S::NOT == 4)                              \
+        (void)hipFuncSetAttribute((const void *)policy_train8_kernel<S>,     \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)train_lds<S>());                      \
       attr = true;                                                           \
     }                                                                        \
-    hipLaunchKernelGGL(policy_train_kernel<S>, dim3(grid), dim3(256),        \
-                       train_lds<S>(), s, a);                                \
+    if constexpr (S::NIT == 4 && S::NOT == 4 && !XH_TRAIN4)                 \
+      hipLaunchKernelGGL(policy_train8_kernel<S>, dim3(grid), dim3(512),     \
+                         train_lds<S>(), s, a);                              \
+    else                                                                     \
+      hipLaunchKernelGGL(policy_train_kernel<S>, dim3(grid), dim3(256),      \
+                         train_lds<S>(), s, a);                              \
     return hipGetLastError();                                                \
   }
   XH_POLICY_SHAPES(X)

@@ -76,6 +76,8 @@ struct PolicyTrainArgs {
   const float *adv;  // [T][N]
   float *slab;       // [gridDim.x][slab_stride]
   int slab_stride;
+  int ablate;        // diagnostics only (XH_ABLATE): bit0 skip dW2, bit1 skip
+                     // dH1/dW1, bit2 skip layer-2 fwd, bit3 skip softmax/loss
 };
 
 struct ValueArgs {

@@ -12,6 +12,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <map>
@@ -85,7 +86,19 @@ struct xh_ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
+  int trainers = 0;      // live trainers on this context
+  bool closing = false;  // xh_ctx_destroy called while trainers were alive
 };
+
+namespace {
+void ctx_free(xh_ctx *c) {
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+}  // namespace
 
 struct timed_event {
   std::string name;
@@ -120,6 +133,7 @@ struct xh_trainer {
   bool need_shift = false;
   bool use_forced = false;
   bool timing = false;
+  bool counted = false;  // holds a reference on ctx
   std::vector<timed_event> events;
   std::vector<void *> allocs;
 
@@ -326,6 +340,10 @@ int do_learn(xh_trainer *t) {
   pa.adv = t->adv;
   pa.slab = t->pslab;
   pa.slab_stride = t->pslab_stride;
+  {
+    const char *ab = std::getenv("XH_ABLATE");  // diagnostics only
+    pa.ablate = ab ? std::atoi(ab) : 0;
+  }
   for (int e = 0; e < c.epochs; ++e) {
     float *g = t->pgrads + (size_t)e * t->np;
     CHK(timed(t, "policy_train", [&]() {
@@ -404,14 +422,16 @@ int xh_ctx_create(int device, int rank, int world, const void *uid128,
   });
 }
 
+// A context outlives its trainers: destroying it with live trainers defers
+// the release to the last xh_trainer_destroy.
 int xh_ctx_destroy(xh_ctx *c) {
   return guard([&]() -> int {
     if (!c) return XH_OK;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
-    if (c->comm) ncclCommDestroy(c->comm);
-    hipStreamDestroy(c->stream);
-    delete c;
+    if (c->trainers > 0) {
+      c->closing = true;
+      return XH_OK;
+    }
+    ctx_free(c);
     return XH_OK;
   });
 }
@@ -569,6 +589,8 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
       xh_trainer_destroy(t);
       return fail(XH_ERR_HIP, "env init: %s", hipGetErrorString(e));
     }
+    t->counted = true;
+    ++ctx->trainers;
     *out = t;
     return XH_OK;
   });
@@ -583,8 +605,11 @@ int xh_trainer_destroy(xh_trainer *t) {
       hipEventDestroy(ev.start);
       hipEventDestroy(ev.stop);
     }
-    for (void *p : t->allocs) hipFree(p);
+    for (void *p : t->allocs) (void)hipFree(p);
+    xh_ctx *c = t->ctx;
+    const bool counted = t->counted;
     delete t;
+    if (counted && --c->trainers == 0 && c->closing) ctx_free(c);
     return XH_OK;
   });
 }
