@@ -55,6 +55,12 @@ struct PShape {
   static constexpr int L_H1 = L_ROLLOUT_END;
   static constexpr int L_DA2 = L_H1 + r4(64 * HS);
   static constexpr int L_TRAIN_END = L_DA2 + r4(64 * AS);
+  // 8-wave kernel: transposed images [feature][row] (row stride 64+4 floats:
+  // conflict-free ds_read_b128 along rows)
+  static constexpr int TS = 68;
+  static constexpr int L_H1T = L_ROLLOUT_END;
+  static constexpr int L_DAT = L_H1T + H1 * TS;
+  static constexpr int L_TRAIN8_END = L_DAT + H2 * TS;
   // end-of-kernel reduction scratch (aliases the H1 / dA2 images)
   static constexpr int RED = H1 * F0 + H1 + 2 * H2 + 1;
   static_assert(4 * RED <= 64 * HS + 64 * AS, "scratch fits");
@@ -639,7 +645,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
 template <class S>
 __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a) {
   static_assert(S::NIT == 4 && S::NOT == 4, "8-wave kernel is for 128x128");
-  static_assert(8 * S::RED <= 64 * S::HS + 64 * S::AS, "scratch fits");
+  static_assert(8 * S::RED <= (S::H1 + S::H2) * S::TS, "scratch fits");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
   __syncthreads();
@@ -650,18 +656,22 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   const int N = a.b.N, T = a.b.T;
   const int gpt = N / S::G;
   const int ngroups = T * gpt;
-  float *H1img = lds + S::L_H1;
-  float *DAimg = lds + S::L_DA2;
+  float *H1T = lds + S::L_H1T;  // [H1][TS]: H1 transposed (feature-major)
+  float *DAT = lds + S::L_DAT;  // [H2][TS]: dL/dA2 transposed
 
   f32x16 accW2[2];
   accW2[0] = zero16();
   accW2[1] = zero16();
-  float accW1[16][S::F0], accB1[16], accW3[16], accB2[16], accB3 = 0.0f;
+  // dW1 columns of the bin features are accumulated per row; the item
+  // features are constant per env and take one of the two table values
+  // (bin_packing.h:73-74), so their columns (and db1) are carried as the
+  // dA1 sums over rows holding item_a (sA) and item_b (sB).
+  float accW1[16][S::D], sA[16], sB[16], accW3[16], accB2[16], accB3 = 0.0f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    accB1[j] = accW3[j] = accB2[j] = 0.0f;
+    sA[j] = sB[j] = accW3[j] = accB2[j] = 0.0f;
 #pragma unroll
-    for (int f = 0; f < S::F0; ++f) accW1[j][f] = 0.0f;
+    for (int f = 0; f < S::D; ++f) accW1[j][f] = 0.0f;
   }
 
   // this lane's row (rt*32 + lr) of the next group is fetched one group
@@ -733,8 +743,9 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         if (it == q) {
 #pragma unroll
           for (int j = 0; j < 16; ++j)
-            H1img[(rt * 32 + lr) * S::HS + it * 32 + acc_row(j, h)] = t1[j];
+            H1T[(it * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = t1[j];
         }
+        if (a.ablate & 4) continue;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
@@ -768,7 +779,9 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const float p = ex / seg_sum<B>(ex);
       const int c = c_cur;
       const float A = A_cur;
-      if (a.algo == kPPO) {
+      if (a.ablate & 8) {
+        gz = z * 1e-3f;
+      } else if (a.algo == kPPO) {
         const float pc = wave_shfl(p, seg0 + c);
         const float ratio = pc / po_cur;
         float clipped = ratio;
@@ -801,41 +814,59 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
           accW3[j] += gr * (v > 0.0f ? v : 0.0f);
           const float d = v > 0.0f ? gr * wq[u] : 0.0f;
           accB2[j] += d;
-          DAimg[(rt * 32 + lr) * S::AS + q * 32 + acc_row(j, h)] = d;
+          DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
         }
       }
     }
     __syncthreads();
 
-    // ---- dW2 tiles (q, 2rt), (q, 2rt+1): K = 64 rows
-#pragma unroll 4
-    for (int s = 0; s < 32; ++s) {
-      const int r = 2 * s + h;
-      const float av = DAimg[r * S::AS + q * 32 + lr];
-      accW2[0] = mfma32(av, H1img[r * S::HS + (2 * rt) * 32 + lr], accW2[0]);
-      accW2[1] = mfma32(av, H1img[r * S::HS + (2 * rt + 1) * 32 + lr], accW2[1]);
+    // ---- dW2 tiles (q, 2rt), (q, 2rt+1): K = 64 rows.  Step s gives lane
+    // half h row 32h + s, so 4 consecutive steps are one ds_read_b128 of a
+    // transposed image row (A: dA2 of H2 unit q*32+lr, B: H1 of unit i).
+    {
+      const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
+      const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
+      const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
+#pragma unroll 1
+      for (int s4 = 0; s4 < ((a.ablate & 1) ? 0 : 8); ++s4) {
+        const float4 av = lds4(pa + 4 * s4);
+        const float4 b0 = lds4(pb0 + 4 * s4);
+        const float4 b1 = lds4(pb1 + 4 * s4);
+        accW2[0] = mfma32(av.x, b0.x, accW2[0]);
+        accW2[1] = mfma32(av.x, b1.x, accW2[1]);
+        accW2[0] = mfma32(av.y, b0.y, accW2[0]);
+        accW2[1] = mfma32(av.y, b1.y, accW2[1]);
+        accW2[0] = mfma32(av.z, b0.z, accW2[0]);
+        accW2[1] = mfma32(av.z, b1.z, accW2[1]);
+        accW2[0] = mfma32(av.w, b0.w, accW2[0]);
+        accW2[1] = mfma32(av.w, b1.w, accW2[1]);
+      }
     }
 
     // ---- dH1 tile q of r-tile rt (K = H2); relu'; dW1, db1
     {
       f32x16 dh = zero16();
 #pragma unroll 8
-      for (int s = 0; s < S::H2 / 2; ++s) {
+      for (int s = 0; s < ((a.ablate & 2) ? 0 : S::H2 / 2); ++s) {
         const int k = 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
-                    DAimg[(rt * 32 + lr) * S::AS + k], dh);
+                    DAT[k * S::TS + rt * 32 + lr], dh);
       }
-      float xf[S::F0];
+      float xf[S::D];
 #pragma unroll
-      for (int f = 0; f < S::F0; ++f) xf[f] = feat(f);
-      const float *hrow = H1img + (rt * 32 + lr) * S::HS + q * 32;
+      for (int f = 0; f < S::D; ++f) xf[f] = feat(f);
+      bool item_is_a = true;
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) item_is_a &= iv_c[d] == a.env.item_a[d];
+      const float *hcol = H1T + (q * 32) * S::TS + rt * 32 + lr;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         // relu' from the H1 image this wave wrote (post-relu > 0 <=> pre > 0)
-        const float d = hrow[acc_row(j, h)] > 0.0f ? dh[j] : 0.0f;
-        accB1[j] += d;
+        const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
+        sA[j] += item_is_a ? d : 0.0f;
+        sB[j] += item_is_a ? 0.0f : d;
 #pragma unroll
-        for (int f = 0; f < S::F0; ++f) accW1[j][f] += d * xf[f];
+        for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
       }
     }
     __syncthreads();
@@ -858,29 +889,35 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       slab[L.oW2() + o2 * S::H1 + it * 32 + lr] = accW2[k][j];
     }
   }
-  float *scr = lds + S::L_H1;  // [8][RED] wave partials (aliases the images)
+  float *scr = lds + S::L_H1T;  // [8][RED] wave partials (aliases the images)
   for (int i = threadIdx.x; i < 8 * S::RED; i += blockDim.x) scr[i] = 0.0f;
   __syncthreads();
   float *my = scr + w * S::RED;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    float vb1 = accB1[j], vw3 = accW3[j], vb2 = accB2[j];
-    float vw1[S::F0];
+    float va = sA[j], vb = sB[j], vw3 = accW3[j], vb2 = accB2[j];
+    float vw1[S::D];
 #pragma unroll
-    for (int f = 0; f < S::F0; ++f) vw1[f] = accW1[j][f];
+    for (int f = 0; f < S::D; ++f) vw1[f] = accW1[j][f];
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) {
-      vb1 += __shfl_xor(vb1, o, kWave);
+      va += __shfl_xor(va, o, kWave);
+      vb += __shfl_xor(vb, o, kWave);
       vw3 += __shfl_xor(vw3, o, kWave);
       vb2 += __shfl_xor(vb2, o, kWave);
 #pragma unroll
-      for (int f = 0; f < S::F0; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
+      for (int f = 0; f < S::D; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
     }
     if (lr == 0) {
       const int i = q * 32 + acc_row(j, h);
 #pragma unroll
-      for (int f = 0; f < S::F0; ++f) my[i * S::F0 + f] = vw1[f];
-      my[S::H1 * S::F0 + i] = vb1;
+      for (int f = 0; f < S::D; ++f) my[i * S::F0 + f] = vw1[f];
+#pragma unroll
+      for (int d = 0; d < S::D; ++d)
+        my[i * S::F0 + S::D + d] =
+            va * ((float)a.env.item_a[d] / (float)kCapacity) +
+            vb * ((float)a.env.item_b[d] / (float)kCapacity);
+      my[S::H1 * S::F0 + i] = va + vb;
       my[S::H1 * S::F0 + S::H1 + i] = vw3;  // o2 = q*32 + acc_row too
       my[S::H1 * S::F0 + S::H1 + S::H2 + i] = vb2;
     }
@@ -929,7 +966,8 @@ constexpr size_t rollout_lds() {
 }
 template <class S>
 constexpr size_t train_lds() {
-  return sizeof(float) * S::L_TRAIN_END;
+  return sizeof(float) *
+         (S::L_TRAIN_END > S::L_TRAIN8_END ? S::L_TRAIN_END : S::L_TRAIN8_END);
 }
 
 bool policy_shape_supported(int B, int D, int H1, int H2) {
