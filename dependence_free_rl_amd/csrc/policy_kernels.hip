@@ -30,7 +30,9 @@ struct PShape {
   static constexpr int F0 = 2 * D;
   static constexpr int S1 = (F0 + 1) / 2;  // layer-1 MFMA k-steps
   static constexpr int NIT = H1 / 32, NOT = H2 / 32;
-  static constexpr int G = 64 / B;  // envs per 64-row group
+  static constexpr int G = B <= 64 ? 64 / B : 1;   // envs per group
+  static constexpr int HG = B <= 64 ? 1 : B / 64;  // 64-row half-groups
+  static constexpr int R = 64 * HG;                // rows per group
   static constexpr int BD = B * D;
   static constexpr int W2S = H1 + 4;           // LDS W2 image row stride
   static constexpr int HS = H1 + 1;            // LDS H1 image row stride
@@ -38,7 +40,7 @@ struct PShape {
   static constexpr int FJ = NOT >= 4 ? 2 : 1;  // fwd r-tiles per wave
   static constexpr int JW = (NOT * NIT + 3) / 4;  // dW2 tiles per wave
   static constexpr int JH = (2 * NIT + 3) / 4;    // dH1 r-tiles per wave
-  static_assert(B == 8 || B == 16 || B == 32 || B == 64, "B");
+  static_assert(B == 8 || B == 16 || B == 32 || B == 64 || B == 128, "B");
   static_assert(NIT == 1 || NIT == 2 || NIT == 4, "H1 in {32,64,128}");
   static_assert(NOT == 1 || NOT == 2 || NOT == 4, "H2 in {32,64,128}");
   static_assert(D >= 1 && D <= 3, "D");
@@ -51,7 +53,7 @@ struct PShape {
   static constexpr int L_W3 = L_B2 + H2;
   static constexpr int L_B3 = L_W3 + H2;
   static constexpr int L_Z = L_B3 + 4;
-  static constexpr int L_ROLLOUT_END = L_Z + NOT * 64;
+  static constexpr int L_ROLLOUT_END = L_Z + NOT * R;
   static constexpr int L_H1 = L_ROLLOUT_END;
   static constexpr int L_DA2 = L_H1 + r4(64 * HS);
   static constexpr int L_TRAIN_END = L_DA2 + r4(64 * AS);
@@ -347,6 +349,149 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
     }
     __syncthreads();
     cur = nxt;
+  }
+}
+
+// ================================================ rollout step, 128 bins ===
+// One env per group (B = 128 = two 64-row half-groups, BASELINE config 5).
+// Forward as rollout_step_kernel per half-group, scores of all 128
+// candidate bins staged in LDS, then wave 0 samples with two bins per lane
+// (bins lane and 64 + lane; sequential discrete_distribution order).
+template <class S>
+__global__ __launch_bounds__(256, 2) void rollout_step128_kernel(RolloutArgs a) {
+  static_assert(S::B == 128 && S::HG == 2, "128-bin rollout");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  constexpr int R = S::R;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31;
+  const int N = a.b.N, t = a.t;
+  const int o2t = w % S::NOT;
+  const int rt0 = S::NOT >= 4 ? 0 : w / S::NOT;
+  const bool fwd_active = (w / S::NOT) * S::FJ < 2;
+  for (int env = blockIdx.x; env < N; env += gridDim.x) {
+#pragma unroll
+    for (int hg = 0; hg < 2; ++hg) {
+      RowRaw<S> rr;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int bin = hg * 64 + k * 32 + lr;
+        const size_t e = (size_t)t * N + env;
+        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
+        const int8_t *ip = a.b.items + e * 4;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          rr.bv[k][d] = bp[d];
+          rr.iv[k][d] = ip[d];
+        }
+      }
+      f32x16 h1[S::NIT][2];
+      layer1<S>(rr, lds, h1);
+      if (fwd_active) {
+        f32x16 pre[S::FJ];
+        layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
+#pragma unroll
+        for (int q = 0; q < S::FJ; ++q) {
+          const float zp = logit_part<S>(lds, pre[q], o2t);
+          if (lane < 32) lds[S::L_Z + o2t * R + hg * 64 + (rt0 + q) * 32 + lr] = zp;
+        }
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      float z[2], p[2];
+      float se = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        float zs = 0.0f;
+#pragma unroll
+        for (int o = 0; o < S::NOT; ++o) zs += lds[S::L_Z + o * R + k * 64 + lane];
+        z[k] = zs + lds[S::L_B3];
+        p[k] = expf(z[k]);
+        se += p[k];
+      }
+      se = seg_sum<64>(se);
+      p[0] = p[0] / se;
+      p[1] = p[1] / se;
+      if (a.logits_out) {
+        a.logits_out[(size_t)env * 128 + lane] = z[0];
+        a.logits_out[(size_t)env * 128 + 64 + lane] = z[1];
+      }
+      if (a.probs_out) {
+        a.probs_out[(size_t)env * 128 + lane] = p[0];
+        a.probs_out[(size_t)env * 128 + 64 + lane] = p[1];
+      }
+      uint32_t x = a.b.rng[env];
+      int choice;
+      if (a.forced) {
+        choice = a.forced[(size_t)t * N + env];
+        (void)canonical(x);
+      } else {
+        const double pd0 = (double)p[0], pd1 = (double)p[1];
+        const double sd = seg_sum_d<64>(pd0 + pd1);
+        const double c0 = seg_scan_d<64>(pd0 / sd, lane);
+        const double tot0 = wave_shfl_d(c0, 63);
+        double c1 = tot0 + seg_scan_d<64>(pd1 / sd, lane);
+        if (lane == 63) c1 = 1.0;
+        const double u = canonical(x);
+        choice = __popcll(__ballot(c0 < u)) + __popcll(__ballot(c1 < u));
+        const float gap = (float)fmin(fabs(c0 - u), fabs(c1 - u));
+        if (seg_min<64>(gap) < 1e-9f) {  // exact sequential restatement
+          double s2 = 0.0;
+          for (int k = 0; k < 128; ++k)
+            s2 += (double)wave_shfl(p[k >> 6], k & 63);
+          double acc = 0.0;
+          int c2 = 127;
+          for (int k = 0; k < 128; ++k) {
+            const double qk = (double)wave_shfl(p[k >> 6], k & 63) / s2;
+            acc = k == 0 ? qk : acc + qk;
+            const double cpk = k == 127 ? 1.0 : acc;
+            if (!(cpk < u) && k < c2) c2 = k;
+          }
+          choice = c2;
+        }
+      }
+      const float pold = choice < 64 ? wave_shfl(p[0], choice)
+                                     : wave_shfl(p[1], choice - 64);
+      const size_t e = (size_t)t * N + env;
+      const int8_t *ip = a.b.items + e * 4;
+      int iv[S::D];
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) iv[d] = ip[d];
+      int nb[2][S::D];
+      int neg[2] = {0, 0};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int bin = k * 64 + lane;
+        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          nb[k][d] = bin == choice ? bp[d] - iv[d] : bp[d];
+          neg[k] |= nb[k][d] < 0;
+        }
+      }
+      const int done = __shfl(choice < 64 ? neg[0] : neg[1], choice & 63, kWave);
+      const bool first = canonical(x) < a.env.p_a;
+      const size_t o = (size_t)(t + 1) * N + env;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        int8_t *ob = a.b.bins + o * S::BD + (k * 64 + lane) * S::D;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d)
+          ob[d] = (int8_t)(done ? kCapacity : nb[k][d]);
+      }
+      if (lane == 0) {
+        int8_t *oi = a.b.items + o * 4;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+        a.b.action[(size_t)t * N + env] = choice;
+        a.b.pold[(size_t)t * N + env] = pold;
+        a.b.done[(size_t)t * N + env] = (uint8_t)done;
+        a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -649,7 +794,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
   __syncthreads();
-  constexpr int B = S::B;
+  constexpr int B = S::B, HG = S::HG, R = S::R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
             h = lane >> 5;
   const int q = w & 3, rt = w >> 2;
@@ -674,13 +819,13 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     for (int f = 0; f < S::D; ++f) accW1[j][f] = 0.0f;
   }
 
-  // this lane's row (rt*32 + lr) of the next group is fetched one group
-  // ahead; its env record (action, p_old, advantage) at the start of the
-  // group it is used in (consumed after the forward pass).
+  // This lane's row (hg*64 + rt*32 + lr) is fetched one group ahead when a
+  // group is one 64-row tile; its env record (action, p_old, advantage) at
+  // the start of the group it is used in (consumed after the forward pass).
   int bv_c[S::D], iv_c[S::D], bv_n[S::D], iv_n[S::D];
-  auto fetch_row = [&](int g, int (&bv)[S::D], int (&iv)[S::D]) {
+  auto fetch_row = [&](int g, int hg, int (&bv)[S::D], int (&iv)[S::D]) {
     const int t = g / gpt, e0 = (g - t * gpt) * S::G;
-    const int r = rt * 32 + lr;
+    const int r = hg * 64 + rt * 32 + lr;
     const size_t env = (size_t)t * N + e0 + r / B;
     const int8_t *bp = a.b.bins + env * S::BD + (r % B) * S::D;
     const int8_t *ip = a.b.items + env * 4;
@@ -690,7 +835,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       iv[d] = ip[d];
     }
   };
-  auto feat = [&](int f) {  // feature f of this lane's row (current group)
+  auto feat = [&](int f) {  // feature f of this lane's row (current tile)
     int v = 0;
 #pragma unroll
     for (int d = 0; d < S::D; ++d) {
@@ -699,181 +844,227 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
     return f < S::F0 ? (float)v / (float)kCapacity : 0.0f;
   };
-  if ((int)blockIdx.x < ngroups) fetch_row(blockIdx.x, bv_c, iv_c);
+  // Layer 1 tile by tile, fused into the layer-2 k-loop, for this wave's
+  // H2 tile q of r-tile rt; optionally writes its H1 tile q to the image.
+  auto forward = [&](bool write_h1) {
+    f32x16 pre = zero16();
+    float xb[S::S1];
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
+    const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      f32x16 t1 = zero16();
+#pragma unroll
+      for (int s = 0; s < S::S1; ++s) {
+        const int k = 2 * s + h;
+        const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+        t1 = mfma32(wa, xb[s], t1);
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float v = t1[4 * qq + u] + bq[u];
+          t1[4 * qq + u] = v > 0.0f ? v : 0.0f;
+        }
+      }
+      if (write_h1 && it == q) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          H1T[(it * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = t1[j];
+      }
+      if (a.ablate & 4) continue;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
+        pre = mfma32(a4.x, t1[4 * qq + 0], pre);
+        pre = mfma32(a4.y, t1[4 * qq + 1], pre);
+        pre = mfma32(a4.z, t1[4 * qq + 2], pre);
+        pre = mfma32(a4.w, t1[4 * qq + 3], pre);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
+      pre[4 * qq + 0] += bb.x;
+      pre[4 * qq + 1] += bb.y;
+      pre[4 * qq + 2] += bb.z;
+      pre[4 * qq + 3] += bb.w;
+    }
+    return pre;
+  };
+
+  if (HG == 1 && (int)blockIdx.x < ngroups) fetch_row(blockIdx.x, 0, bv_c, iv_c);
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int gn = g + gridDim.x;
-    if (gn < ngroups) fetch_row(gn, bv_n, iv_n);
+    if (HG == 1 && gn < ngroups) fetch_row(gn, 0, bv_n, iv_n);
     int c_cur;
     float po_cur, A_cur;
     {
       const int t = g / gpt, e0 = (g - t * gpt) * S::G;
-      const size_t ti = (size_t)t * N + e0 + lane / B;
+      const size_t ti = (size_t)t * N + e0 + lane / (B <= 64 ? B : 64);
       c_cur = a.b.action[ti];
       po_cur = a.b.pold[ti];
       A_cur = a.adv[ti];
     }
 
-    // ---- layer 1 tile by tile, fused into the layer-2 k-loop
-    f32x16 pre = zero16();
-    {
-      float xb[S::S1];
+    // ---- forward (all R rows) -> per-tile partial logits in LDS
+    f32x16 pre;
 #pragma unroll
-      for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
-      const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        f32x16 t1 = zero16();
-#pragma unroll
-        for (int s = 0; s < S::S1; ++s) {
-          const int k = 2 * s + h;
-          const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
-          t1 = mfma32(wa, xb[s], t1);
-        }
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
-          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float v = t1[4 * qq + u] + bq[u];
-            t1[4 * qq + u] = v > 0.0f ? v : 0.0f;
-          }
-        }
-        if (it == q) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            H1T[(it * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = t1[j];
-        }
-        if (a.ablate & 4) continue;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
-          pre = mfma32(a4.x, t1[4 * qq + 0], pre);
-          pre = mfma32(a4.y, t1[4 * qq + 1], pre);
-          pre = mfma32(a4.z, t1[4 * qq + 2], pre);
-          pre = mfma32(a4.w, t1[4 * qq + 3], pre);
-        }
-      }
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
-        pre[4 * qq + 0] += bb.x;
-        pre[4 * qq + 1] += bb.y;
-        pre[4 * qq + 2] += bb.z;
-        pre[4 * qq + 3] += bb.w;
-      }
+    for (int hg = 0; hg < HG; ++hg) {
+      if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
+      pre = forward(HG == 1);
       const float zp = logit_part<S>(lds, pre, q);
-      if (lane < 32) lds[S::L_Z + q * 64 + rt * 32 + lr] = zp;
+      if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
     }
     __syncthreads();
 
-    // ---- logits -> softmax -> loss gradient w.r.t. logits (lane = row)
-    float gz;
+    // ---- logits -> softmax -> loss gradient w.r.t. logits; lane holds the
+    // rows lane + 64*k (k < HG)
+    float gzk[HG];
     {
-      const int bin = lane % B, seg0 = (lane / B) * B;
-      const float zs = ((lds[S::L_Z + lane] + lds[S::L_Z + 64 + lane]) +
-                        lds[S::L_Z + 128 + lane]) + lds[S::L_Z + 192 + lane];
-      const float z = zs + lds[S::L_B3];
-      const float ex = expf(z);
-      const float p = ex / seg_sum<B>(ex);
+      constexpr int SEG = B <= 64 ? B : 64;
+      float z[HG], ex[HG], p[HG];
+      float se = 0.0f;
+#pragma unroll
+      for (int k = 0; k < HG; ++k) {
+        const int r = k * 64 + lane;
+        const float zs = ((lds[S::L_Z + r] + lds[S::L_Z + R + r]) +
+                          lds[S::L_Z + 2 * R + r]) + lds[S::L_Z + 3 * R + r];
+        z[k] = zs + lds[S::L_B3];
+        ex[k] = expf(z[k]);
+        se += ex[k];
+      }
+      se = seg_sum<SEG>(se);
+#pragma unroll
+      for (int k = 0; k < HG; ++k) p[k] = ex[k] / se;
       const int c = c_cur;
       const float A = A_cur;
-      if (a.ablate & 8) {
-        gz = z * 1e-3f;
-      } else if (a.algo == kPPO) {
-        const float pc = wave_shfl(p, seg0 + c);
-        const float ratio = pc / po_cur;
-        float clipped = ratio;
-        if (ratio > 1.0f + a.clip_eps)
-          clipped = 1.0f + a.clip_eps;
-        else if (ratio < 1.0f - a.clip_eps)
-          clipped = 1.0f - a.clip_eps;
-        const float ig = fminf(clipped * A, ratio * A) * -1.0f;
-        const float gc = ig / pc;
-        const float lin = bin == c ? p : 0.0f;
-        gz = (lin - p * pc) * gc;
-      } else {
-        gz = p * A;
-        if (bin == c) gz -= A;
+      const int seg0 = (lane / SEG) * SEG;
+      // p of the chosen bin (bin c lives in lane c % 64 of row block c / 64)
+      float pc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < HG; ++k) {
+        const float v = wave_shfl(p[k], seg0 + (c % SEG));
+        if (HG == 1 || c / 64 == k) pc = v;
       }
-      if (w == 0) accB3 += gz;
+#pragma unroll
+      for (int k = 0; k < HG; ++k) {
+        const int bin = (k * 64 + lane) % B;
+        float gz;
+        if (a.ablate & 8) {
+          gz = z[k] * 1e-3f;
+        } else if (a.algo == kPPO) {
+          // clipped_gradient (rl.h:54-74) + softmax_layer::backward
+          // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
+          const float ratio = pc / po_cur;
+          float clipped = ratio;
+          if (ratio > 1.0f + a.clip_eps)
+            clipped = 1.0f + a.clip_eps;
+          else if (ratio < 1.0f - a.clip_eps)
+            clipped = 1.0f - a.clip_eps;
+          const float ig = fminf(clipped * A, ratio * A) * -1.0f;
+          const float gc = ig / pc;
+          const float lin = bin == c ? p[k] : 0.0f;
+          gz = (lin - p[k] * pc) * gc;
+        } else {
+          // softmax_gradient_log (rl.h:45-52) through softmax-xent (identity)
+          gz = p[k] * A;
+          if (bin == c) gz -= A;
+        }
+        gzk[k] = gz;
+        if (w == 0) accB3 += gz;
+      }
     }
 
-    // ---- backward through layer 3 and the layer-2 relu (tile q, r-tile rt)
-    {
-      const float gr = wave_shfl(gz, rt * 32 + lr);
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
-        const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+    for (int hg = 0; hg < HG; ++hg) {
+      if (HG > 1) {  // recompute this half-group's forward (no room to keep it)
+        if (hg > 0) __syncthreads();  // previous half-group's images consumed
+        fetch_row(g, hg, bv_c, iv_c);
+        pre = forward(true);
+      }
+      // ---- backward through layer 3 and the layer-2 relu
+      {
+        const float gr = wave_shfl(gzk[hg], rt * 32 + lr);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = 4 * qq + u;
-          const float v = pre[j];
-          accW3[j] += gr * (v > 0.0f ? v : 0.0f);
-          const float d = v > 0.0f ? gr * wq[u] : 0.0f;
-          accB2[j] += d;
-          DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
+        for (int qq = 0; qq < 4; ++qq) {
+          const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
+          const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = 4 * qq + u;
+            const float v = pre[j];
+            accW3[j] += gr * (v > 0.0f ? v : 0.0f);
+            const float d = v > 0.0f ? gr * wq[u] : 0.0f;
+            accB2[j] += d;
+            DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
+          }
+        }
+      }
+      __syncthreads();
+
+      // ---- dW2 tiles (q, 2rt), (q, 2rt+1): K = 64 rows.  Step s gives lane
+      // half h row 32h + s, so 4 consecutive steps are one ds_read_b128 of a
+      // transposed image row (A: dA2 of H2 unit q*32+lr, B: H1 of unit i).
+      {
+        const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
+        const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
+        const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
+#pragma unroll 1
+        for (int s4 = 0; s4 < ((a.ablate & 1) ? 0 : 8); ++s4) {
+          const float4 av = lds4(pa + 4 * s4);
+          const float4 b0 = lds4(pb0 + 4 * s4);
+          const float4 b1 = lds4(pb1 + 4 * s4);
+          accW2[0] = mfma32(av.x, b0.x, accW2[0]);
+          accW2[1] = mfma32(av.x, b1.x, accW2[1]);
+          accW2[0] = mfma32(av.y, b0.y, accW2[0]);
+          accW2[1] = mfma32(av.y, b1.y, accW2[1]);
+          accW2[0] = mfma32(av.z, b0.z, accW2[0]);
+          accW2[1] = mfma32(av.z, b1.z, accW2[1]);
+          accW2[0] = mfma32(av.w, b0.w, accW2[0]);
+          accW2[1] = mfma32(av.w, b1.w, accW2[1]);
+        }
+      }
+
+      // ---- dH1 tile q of r-tile rt (K = H2); relu'; dW1, db1
+      {
+        f32x16 dh = zero16();
+#pragma unroll 8
+        for (int s = 0; s < ((a.ablate & 2) ? 0 : S::H2 / 2); ++s) {
+          const int k = 2 * s + h;
+          dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
+                      DAT[k * S::TS + rt * 32 + lr], dh);
+        }
+        float xf[S::D];
+#pragma unroll
+        for (int f = 0; f < S::D; ++f) xf[f] = feat(f);
+        bool item_is_a = true;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) item_is_a &= iv_c[d] == a.env.item_a[d];
+        const float *hcol = H1T + (q * 32) * S::TS + rt * 32 + lr;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          // relu' from the H1 image (post-relu > 0 <=> pre > 0)
+          const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
+          sA[j] += item_is_a ? d : 0.0f;
+          sB[j] += item_is_a ? 0.0f : d;
+#pragma unroll
+          for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
         }
       }
     }
     __syncthreads();
-
-    // ---- dW2 tiles (q, 2rt), (q, 2rt+1): K = 64 rows.  Step s gives lane
-    // half h row 32h + s, so 4 consecutive steps are one ds_read_b128 of a
-    // transposed image row (A: dA2 of H2 unit q*32+lr, B: H1 of unit i).
-    {
-      const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
-      const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
-      const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
-#pragma unroll 1
-      for (int s4 = 0; s4 < ((a.ablate & 1) ? 0 : 8); ++s4) {
-        const float4 av = lds4(pa + 4 * s4);
-        const float4 b0 = lds4(pb0 + 4 * s4);
-        const float4 b1 = lds4(pb1 + 4 * s4);
-        accW2[0] = mfma32(av.x, b0.x, accW2[0]);
-        accW2[1] = mfma32(av.x, b1.x, accW2[1]);
-        accW2[0] = mfma32(av.y, b0.y, accW2[0]);
-        accW2[1] = mfma32(av.y, b1.y, accW2[1]);
-        accW2[0] = mfma32(av.z, b0.z, accW2[0]);
-        accW2[1] = mfma32(av.z, b1.z, accW2[1]);
-        accW2[0] = mfma32(av.w, b0.w, accW2[0]);
-        accW2[1] = mfma32(av.w, b1.w, accW2[1]);
+    if (HG == 1) {
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) {
+        bv_c[d] = bv_n[d];
+        iv_c[d] = iv_n[d];
       }
-    }
-
-    // ---- dH1 tile q of r-tile rt (K = H2); relu'; dW1, db1
-    {
-      f32x16 dh = zero16();
-#pragma unroll 8
-      for (int s = 0; s < ((a.ablate & 2) ? 0 : S::H2 / 2); ++s) {
-        const int k = 2 * s + h;
-        dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
-                    DAT[k * S::TS + rt * 32 + lr], dh);
-      }
-      float xf[S::D];
-#pragma unroll
-      for (int f = 0; f < S::D; ++f) xf[f] = feat(f);
-      bool item_is_a = true;
-#pragma unroll
-      for (int d = 0; d < S::D; ++d) item_is_a &= iv_c[d] == a.env.item_a[d];
-      const float *hcol = H1T + (q * 32) * S::TS + rt * 32 + lr;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        // relu' from the H1 image this wave wrote (post-relu > 0 <=> pre > 0)
-        const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
-        sA[j] += item_is_a ? d : 0.0f;
-        sB[j] += item_is_a ? 0.0f : d;
-#pragma unroll
-        for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int d = 0; d < S::D; ++d) {
-      bv_c[d] = bv_n[d];
-      iv_c[d] = iv_n[d];
     }
   }
 
@@ -954,7 +1145,8 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   X(8, 2, 64, 32)           \
   X(16, 2, 64, 64)          \
   X(32, 1, 64, 64)          \
-  X(64, 2, 128, 128)
+  X(64, 2, 128, 128)        \
+  X(128, 3, 128, 128)
 
 #ifndef XH_TRAIN4
 #define XH_TRAIN4 0  // 1: force the 4-wave train kernel everywhere (A/B)
@@ -1008,14 +1200,24 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
     using S = PShape<XB, XD, XH1, XH2>;                                      \
     static bool attr = false;                                                \
     if (!attr) {                                                             \
-      (void)hipFuncSetAttribute((const void *)rollout_step_kernel<S>,        \
-                                hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                                (int)rollout_lds<S>());                      \
+      if constexpr (S::HG == 1)                                              \
+        (void)hipFuncSetAttribute((const void *)rollout_step_kernel<S>,      \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)rollout_lds<S>());                    \
+      else                                                                   \
+        (void)hipFuncSetAttribute((const void *)rollout_step128_kernel<S>,   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)rollout_lds<S>());                    \
       attr = true;                                                           \
     }                                                                        \
     const int ng = a.b.N / S::G;                                             \
-    hipLaunchKernelGGL(rollout_step_kernel<S>, dim3(grid < ng ? grid : ng),  \
-                       dim3(256), rollout_lds<S>(), s, a);                   \
+    if constexpr (S::HG == 1)                                                \
+      hipLaunchKernelGGL(rollout_step_kernel<S>, dim3(grid < ng ? grid : ng),\
+                         dim3(256), rollout_lds<S>(), s, a);                 \
+    else                                                                     \
+      hipLaunchKernelGGL(rollout_step128_kernel<S>,                          \
+                         dim3(grid < ng ? grid : ng), dim3(256),             \
+                         rollout_lds<S>(), s, a);                            \
     return hipGetLastError();                                                \
   }
   XH_POLICY_SHAPES(X)
@@ -1031,19 +1233,20 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
     using S = PShape<XB, XD, XH1, XH2>;                                      \
     static bool attr = false;                                                \
     if (!attr) {                                                             \
-      (void)hipFuncSetAttribute((const void *)policy_train_kernel<S>,        \
-                                hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                                (int)train_lds<S>());                        \
+      if constexpr (S::HG == 1)                                              \
+        (void)hipFuncSetAttribute((const void *)policy_train_kernel<S>,      \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)train_lds<S>());                      \
       if constexpr (S::NIT == 4 && S::NOT == 4)                              \
         (void)hipFuncSetAttribute((const void *)policy_train8_kernel<S>,     \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,\
                                   (int)train_lds<S>());                      \
       attr = true;                                                           \
     }                                                                        \
-    if constexpr (S::NIT == 4 && S::NOT == 4 && !XH_TRAIN4)                 \
+    if constexpr (S::NIT == 4 && S::NOT == 4 && (!XH_TRAIN4 || S::HG > 1))  \
       hipLaunchKernelGGL(policy_train8_kernel<S>, dim3(grid), dim3(512),     \
                          train_lds<S>(), s, a);                              \
-    else                                                                     \
+    else if constexpr (S::HG == 1)                                           \
       hipLaunchKernelGGL(policy_train_kernel<S>, dim3(grid), dim3(256),      \
                          train_lds<S>(), s, a);                              \
     return hipGetLastError();                                                \

@@ -498,7 +498,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     if (!xh::value_shape_supported(c.value_h1, c.value_h2))
       return fail(XH_ERR_INVALID, "unsupported value widths [%d,%d]",
                   c.value_h1, c.value_h2);
-    const int G = 64 / c.bins;
+    const int G = c.bins <= 64 ? 64 / c.bins : 1;  // envs per 64-row group
     if (c.num_envs <= 0 || c.num_envs % G)
       return fail(XH_ERR_INVALID, "num_envs %d must be a positive multiple of %d",
                   c.num_envs, G);

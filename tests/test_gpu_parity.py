@@ -25,7 +25,7 @@ def ctx():
     c.close()
 
 
-ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2"]
+ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3"]
 
 
 @pytest.mark.parametrize("name", ENV_CASES)
@@ -77,7 +77,7 @@ def test_rollout_teacher_forced_bit_exact(ctx, name):
         tr.learn()  # advance the batch window (forget())
 
 
-@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "ppo_b64d2"])
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "ppo_b64d2", "ac_b128d3"])
 def test_rollout_sampling_matches_reference(ctx, name):
     """Free-running: the GPU's own softmax + categorical sampler picks the
     reference's actions (no fixture step lies on a probability near-tie)."""
@@ -96,7 +96,8 @@ def test_rollout_sampling_matches_reference(ctx, name):
         tr.learn()
 
 
-@pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2"])
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2",
+                                  "ac_b128d3"])
 def test_learn_matches_reference(ctx, name):
     """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
     value gradient and updated parameters vs the reference learner."""

@@ -31,6 +31,7 @@ def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     ("ppo", 64, 2, (128, 128), 32, 4),   # BASELINE config 3 shape
     ("ppo", 32, 1, (64, 64), 64, 4),     # config 2 shape
     ("ac", 16, 2, (64, 64), 64, 8),
+    ("ac", 128, 3, (128, 128), 8, 8),    # config 5 shape
 ])
 def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
     from oracle import pyoracle as po
