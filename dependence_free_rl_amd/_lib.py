@@ -64,6 +64,7 @@ def _load():
         "xh_trainer_buffer_bytes": (sz, [vp, i]),
         "xh_trainer_get_buffer": (i, [vp, i, vp, sz]),
         "xh_trainer_set_buffer": (i, [vp, i, vp, sz]),
+        "xh_trainer_evaluate": (i, [vp, i, i, C.c_uint32, i, vp, vp]),
         "xh_trainer_set_timing": (i, [vp, i]),
         "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_long)]),

@@ -495,6 +495,136 @@ __global__ __launch_bounds__(256, 2) void rollout_step128_kernel(RolloutArgs a) 
   }
 }
 
+// ======================================================= argmax evaluation ==
+// Whole episodes inside one launch: the G envs of a group keep their state in
+// LDS and step until each has finished `episodes` episodes (argmax action: no
+// sampling draws, 2 engine draws per step for the item / reset).
+template <class S>
+__global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
+  static_assert(S::HG == 1, "groups of whole envs");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  constexpr int B = S::B, G = S::G, D = S::D;
+  int *sbins = reinterpret_cast<int *>(lds + S::L_ROLLOUT_END);  // [G][B*D]
+  int *sitem = sbins + G * S::BD;                                // [G][4]
+  uint32_t *srng = reinterpret_cast<uint32_t *>(sitem + G * 4);  // [G]
+  int *sleft = reinterpret_cast<int *>(srng + G);                // [G]
+  int *sflag = sleft + G;                                        // [1]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int o2t = w % S::NOT;
+  const int rt0 = S::NOT >= 4 ? 0 : w / S::NOT;
+  const bool fwd_active = (w / S::NOT) * S::FJ < 2;
+  const int ngroups = a.n_envs / G;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    __syncthreads();
+    if (w == 0) {  // construct: bins at capacity, one item (2 draws)
+      const int e = lane / B, bin = lane % B, env = g * G + e;
+      uint32_t x = mstd_jump(a.x0, (uint64_t)env * a.stream_stride);
+      const bool first = canonical(x) < a.env.p_a;
+      for (int d = 0; d < D; ++d) sbins[e * S::BD + bin * D + d] = kCapacity;
+      if (bin == 0) {
+        for (int d = 0; d < 4; ++d)
+          sitem[e * 4 + d] = d < D ? (first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+        srng[e] = x;
+        sleft[e] = a.episodes;
+        a.total[env] = 0.0;
+        a.steps[env] = 0;
+      }
+    }
+    __syncthreads();
+    double reward = 0.0;  // per segment leader
+    long nsteps = 0;
+    for (long it = 0; it < a.max_steps; ++it) {
+      RowRaw<S> rr;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int r = rt * 32 + lr, e = r / B, bin = r % B;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          rr.bv[rt][d] = sbins[e * S::BD + bin * D + d];
+          rr.iv[rt][d] = sitem[e * 4 + d];
+        }
+      }
+      {
+        f32x16 h1[S::NIT][2];
+        layer1<S>(rr, lds, h1);
+        if (fwd_active) {
+          f32x16 pre[S::FJ];
+          layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
+#pragma unroll
+          for (int q = 0; q < S::FJ; ++q) {
+            const float zp = logit_part<S>(lds, pre[q], o2t);
+            if (lane < 32) lds[S::L_Z + o2t * 64 + (rt0 + q) * 32 + lr] = zp;
+          }
+        }
+      }
+      __syncthreads();
+      if (w == 0) {
+        const int e = lane / B, bin = lane % B, seg0 = e * B;
+        float zs = 0.0f;
+#pragma unroll
+        for (int o = 0; o < S::NOT; ++o) zs += lds[S::L_Z + o * 64 + lane];
+        float v = zs + lds[S::L_B3];
+        if (a.argmax_probs) {
+          const float ex = expf(v);
+          v = ex / seg_sum<B>(ex);
+        }
+        // std::ranges::max_element: first maximum (tensor.cc:464-466)
+        float bv = v;
+        int bi = bin;
+#pragma unroll
+        for (int o = 1; o < B; o <<= 1) {
+          const float ov = __shfl_xor(bv, o, kWave);
+          const int oi = __shfl_xor(bi, o, kWave);
+          if (ov > bv || (ov == bv && oi < bi)) {
+            bv = ov;
+            bi = oi;
+          }
+        }
+        const int choice = bi;
+        const bool active = sleft[e] > 0;
+        int nb[D];
+        int neg = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const int b0 = sbins[e * S::BD + bin * D + d];
+          nb[d] = bin == choice ? b0 - sitem[e * 4 + d] : b0;
+          neg |= nb[d] < 0;
+        }
+        const int done = __shfl(neg, seg0 + choice, kWave);
+        if (active) {
+          uint32_t x = srng[e];
+          const bool first = canonical(x) < a.env.p_a;  // get_item / reset
+#pragma unroll
+          for (int d = 0; d < D; ++d)
+            sbins[e * S::BD + bin * D + d] = done ? kCapacity : nb[d];
+          // all lanes of the segment read srng/sitem above before this write
+          __builtin_amdgcn_wave_barrier();
+          if (bin == 0) {
+            for (int d = 0; d < D; ++d)
+              sitem[e * 4 + d] = first ? a.env.item_a[d] : a.env.item_b[d];
+            srng[e] = x;
+            if (done) sleft[e] -= 1;
+            reward += done ? 0.0 : 1.0;
+            ++nsteps;
+          }
+        }
+        // sleft was updated above by this wave's segment leaders
+        const int any = __any(sleft[e] > 0);
+        if (lane == 0) *sflag = any;
+      }
+      __syncthreads();
+      if (*sflag == 0) break;
+    }
+    if (w == 0 && lane % B == 0) {
+      const int env = g * G + lane / B;
+      a.total[env] = reward;
+      a.steps[env] = nsteps;
+    }
+  }
+}
+
 // ============================================================ train epoch ==
 template <class S>
 __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a) {
@@ -1219,6 +1349,33 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                          dim3(grid < ng ? grid : ng), dim3(256),             \
                          rollout_lds<S>(), s, a);                            \
     return hipGetLastError();                                                \
+  }
+  XH_POLICY_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
+                              hipStream_t s) {
+  const int B = a.env.B, D = a.env.D;
+#define X(XB, XD, XH1, XH2)                                                  \
+  if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
+    using S = PShape<XB, XD, XH1, XH2>;                                      \
+    if constexpr (S::HG == 1) {                                              \
+      constexpr size_t bytes =                                               \
+          rollout_lds<S>() + sizeof(int) * (S::G * (S::BD + 4 + 2) + 4);     \
+      static bool attr = false;                                              \
+      if (!attr) {                                                           \
+        (void)hipFuncSetAttribute((const void *)eval_argmax_kernel<S>,       \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)bytes);                               \
+        attr = true;                                                         \
+      }                                                                      \
+      const int ng = a.n_envs / S::G;                                        \
+      hipLaunchKernelGGL(eval_argmax_kernel<S>,                              \
+                         dim3(ng < 1024 ? ng : 1024), dim3(256), bytes, s, a);\
+      return hipGetLastError();                                              \
+    }                                                                        \
   }
   XH_POLICY_SHAPES(X)
 #undef X

@@ -97,6 +97,23 @@ struct ValueArgs {
   float *row_d2;         // [T*N][V2]
 };
 
+// Deterministic (argmax) evaluation, policy_gradient_deterministic_policy
+// (policy_gradient.h:356-373) as used by deep_agent.cc and the drivers'
+// every-100-iterations evaluation: `episodes` whole episodes per env, env e
+// on its own minstd stream starting at jump(x0, e * stream_stride).
+struct EvalArgs {
+  EnvDesc env;
+  const float *params;
+  int n_envs;
+  int episodes;
+  int argmax_probs;  // 1: argmax over softmax output, 0: over raw logits
+  uint32_t x0;
+  uint64_t stream_stride;
+  long max_steps;     // safety bound per env
+  double *total;      // [n_envs] summed rewards
+  long *steps;        // [n_envs] env steps taken
+};
+
 // Launchers (return hipError_t of the launch). `variant` selects the
 // <B,D,H1,H2> instantiation; returns hipErrorInvalidValue when unsupported.
 bool policy_shape_supported(int B, int D, int H1, int H2);
@@ -107,6 +124,8 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                int grid, hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2);
+hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
+                              hipStream_t s);
 int rollout_grid(int B, int D, int H1, int H2);
 
 bool value_shape_supported(int V1, int V2);

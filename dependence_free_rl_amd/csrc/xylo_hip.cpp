@@ -742,6 +742,58 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
   });
 }
 
+int xh_trainer_evaluate(xh_trainer *t, int n_envs, int episodes,
+                        uint32_t rng_state, int argmax_probs, double *totals,
+                        long *steps) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    const int G = t->cfg.bins <= 64 ? 64 / t->cfg.bins : 0;
+    if (G == 0)
+      return fail(XH_ERR_INVALID, "evaluate: bins %d > 64 not supported",
+                  t->cfg.bins);
+    if (n_envs <= 0 || n_envs % G || episodes < 0)
+      return fail(XH_ERR_INVALID, "evaluate: n_envs %d (multiple of %d), "
+                  "episodes %d", n_envs, G, episodes);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    hipStream_t s = t->ctx->stream;
+    double *dtot = nullptr;
+    long *dsteps = nullptr;
+    HIPCHK(hipMallocAsync((void **)&dtot, sizeof(double) * n_envs, s));
+    HIPCHK(hipMallocAsync((void **)&dsteps, sizeof(long) * n_envs, s));
+    xh::EvalArgs a{};
+    a.env = t->env;
+    a.params = t->pp;
+    a.n_envs = n_envs;
+    a.episodes = episodes;
+    a.argmax_probs = argmax_probs ? 1 : 0;
+    uint32_t x0 = rng_state % 2147483647u;
+    a.x0 = x0 ? x0 : 1u;
+    a.stream_stride = 1ull << 26;
+    // an episode lasts at most B * capacity * D + 1 steps (every step puts
+    // at least one unit into some bin)
+    a.max_steps = (long)(episodes + 1) * (t->cfg.bins * 8 * t->cfg.dims + 2);
+    a.total = dtot;
+    a.steps = dsteps;
+    int st = timed(t, "evaluate", [&]() {
+      return xh::launch_eval_argmax(a, t->cfg.policy_h1, t->cfg.policy_h2, s);
+    });
+    if (st == XH_OK && totals)
+      st = hipMemcpyAsync(totals, dtot, sizeof(double) * n_envs,
+                          hipMemcpyDeviceToHost, s) == hipSuccess
+               ? XH_OK
+               : fail(XH_ERR_HIP, "evaluate: copy");
+    if (st == XH_OK && steps)
+      st = hipMemcpyAsync(steps, dsteps, sizeof(long) * n_envs,
+                          hipMemcpyDeviceToHost, s) == hipSuccess
+               ? XH_OK
+               : fail(XH_ERR_HIP, "evaluate: copy");
+    (void)hipFreeAsync(dtot, s);
+    (void)hipFreeAsync(dsteps, s);
+    HIPCHK(hipStreamSynchronize(s));
+    return st;
+  });
+}
+
 int xh_trainer_set_timing(xh_trainer *t, int on) {
   if (!t) return fail(XH_ERR_INVALID, "null trainer");
   t->timing = on != 0;

@@ -202,6 +202,16 @@ class Trainer:
         a = np.ascontiguousarray(arr, dt).reshape(shape)
         check(_lib.lib.xh_trainer_set_buffer(self.h, which, _ptr(a), a.nbytes))
 
+    def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False):
+        """Argmax evaluation (deep_agent.cc / the drivers' periodic eval):
+        returns (total reward per env, env steps per env)."""
+        tot = np.zeros(n_envs, np.float64)
+        steps = np.zeros(n_envs, np.int64)
+        check(_lib.lib.xh_trainer_evaluate(self.h, n_envs, episodes, rng_state,
+                                           1 if argmax_probs else 0, _ptr(tot),
+                                           _ptr(steps)))
+        return tot, steps
+
     # ------------------------------------------------------------ timing --
     def set_timing(self, on):
         check(_lib.lib.xh_trainer_set_timing(self.h, 1 if on else 0))

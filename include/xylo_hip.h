@@ -129,6 +129,18 @@ int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes);
 int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
                           size_t bytes);
 
+/* Deterministic evaluation (policy_gradient_deterministic_policy,
+ * policy_gradient.h:356-373; deep_agent.cc:25-41; the drivers' 100-episode
+ * eval, ppo_training.cc:67-81) with the trainer's current policy: n_envs
+ * independent envs (multiple of 64/bins) each play `episodes` whole episodes,
+ * argmax action (over the softmax output if argmax_probs, else the logits).
+ * Env e's minstd_rand0 stream starts at rng_state advanced by e * 2^26 draws,
+ * so env 0 reproduces a single-env reference run seeded at rng_state.
+ * totals/steps (host, n_envs each, may be NULL): summed rewards, env steps. */
+int xh_trainer_evaluate(xh_trainer *t, int n_envs, int episodes,
+                        uint32_t rng_state, int argmax_probs, double *totals,
+                        long *steps);
+
 /* Kernel timing with HIP events on the trainer's stream (off by default). */
 int xh_trainer_set_timing(xh_trainer *t, int on);
 /* name: "rollout_step" | "policy_train" | "value" | "reduce_sgd" | "allreduce"

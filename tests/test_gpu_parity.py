@@ -158,3 +158,21 @@ def test_weights20_logits(ctx):
     z = tr.buffer(BUF_LOGITS)
     assert_close(z, g["logits"], what="weights.20 logits")
     assert abs(z[0, 0] - 2.76766) < 1e-4 and np.allclose(z[0], z[0, 0], atol=1e-6)
+
+
+def test_deep_agent_argmax_episodes(ctx):
+    """deep_agent.cc: weights.20, seed 1, 1000 argmax episodes -> total reward
+    26600 (apps/bin_packing/deep_agent.cc:21-41), every episode length equal
+    to the reference's; the other 7 envs of the group run on their own
+    streams."""
+    from dependence_free_rl_amd import Trainer
+    from dependence_free_rl_amd.trainer import POLICY
+    g = golden("deep_w20")
+    tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1,
+                 widths=(128, 64))
+    tr.set_params(POLICY, g["params"])
+    tot, steps = tr.evaluate(8, 1000, int(g["x0"][0]))
+    assert tot[0] == float(g["total_reward"][0]) == 26600.0
+    assert steps[0] == int(g["episode_len"].sum()) == 27600
+    # 26.55 +/- 0.03 average (deep.log) for the independent streams too
+    assert np.all(np.abs(tot / 1000.0 - 26.55) < 0.5)
