@@ -13,8 +13,22 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/xylo_hip.o
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h include/xylo_hip.h
 
-.PHONY: all lib oracle clean
-all: lib oracle
+# Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
+# apps/bin_packing drivers (when the reference tree is present) and our own
+# examples/ drivers, compiled against it and linked to the library.
+CXX20    ?= /opt/rocm/lib/llvm/bin/clang++
+REF      ?= /root/reference
+COMPAT   := build/compat
+CXXFLAGS20 := -std=c++20 -O2 -Wall -Wno-unused-variable -Iinclude/xylo_compat \
+              -Iinclude
+LDCOMPAT := -L$(PKG) -lxylo_hip -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+REF_APPS := ppo_training ac_training ppo2_training pg_training deep_agent \
+            random_agent firstfit_agent bestfit_agent minwaste_agent
+EXAMPLES := $(patsubst examples/%.cc,$(COMPAT)/%,$(wildcard examples/*.cc))
+COMPAT_HDRS := $(shell find include/xylo_compat -name '*.h') include/xylo_hip.h
+
+.PHONY: all lib oracle compat clean
+all: lib oracle compat
 
 lib: $(LIB)
 
@@ -31,6 +45,18 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle port
 	@if [ -d /root/reference ]; then $(MAKE) -C oracle ref; fi
+
+compat: $(EXAMPLES)
+	@mkdir -p $(COMPAT)
+	@if [ -d $(REF)/apps/bin_packing ]; then \
+	  for a in $(REF_APPS); do \
+	    $(CXX20) $(CXXFLAGS20) -Wno-logical-op-parentheses \
+	      $(REF)/apps/bin_packing/$$a.cc $(LDCOMPAT) -o $(COMPAT)/$$a || exit 1; \
+	  done; fi
+
+$(COMPAT)/%: examples/%.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
 
 clean:
 	rm -f $(OBJS) $(LIB)

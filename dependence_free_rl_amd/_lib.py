@@ -36,6 +36,16 @@ class Config(C.Structure):
         ("rng_state", C.c_uint32)]
 
 
+class Eval(C.Structure):
+    """Mirror of xh_eval."""
+    _fields_ = [
+        ("n_envs", C.c_int), ("episodes", C.c_int), ("argmax_probs", C.c_int),
+        ("rng_state", C.c_uint32), ("init_items", C.c_void_p),
+        ("final_items", C.c_void_p), ("rng_out", C.c_void_p),
+        ("totals", C.c_void_p), ("steps", C.c_void_p), ("trace", C.c_void_p),
+        ("trace_cap", C.c_long)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -64,7 +74,8 @@ def _load():
         "xh_trainer_buffer_bytes": (sz, [vp, i]),
         "xh_trainer_get_buffer": (i, [vp, i, vp, sz]),
         "xh_trainer_set_buffer": (i, [vp, i, vp, sz]),
-        "xh_trainer_evaluate": (i, [vp, i, i, C.c_uint32, i, vp, vp]),
+        "xh_trainer_evaluate": (i, [vp, C.POINTER(Eval)]),
+        "xh_trainer_seed_streams": (i, [vp, C.c_uint32]),
         "xh_trainer_set_timing": (i, [vp, i]),
         "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_long)]),

@@ -39,4 +39,19 @@ hipError_t launch_env_init(const EnvDesc &env, Batch b, uint32_t x0,
   return hipGetLastError();
 }
 
+// xh_trainer_seed_streams: window-start stream of env g = x advanced 4*T*g.
+__global__ void env_seed_kernel(Batch b, uint32_t x, int env_offset) {
+  for (int env = blockIdx.x * blockDim.x + threadIdx.x; env < b.N;
+       env += gridDim.x * blockDim.x)
+    b.rng[env] = mstd_jump(x, 4ull * b.T * ((uint64_t)env_offset + env));
+}
+
+hipError_t launch_env_seed(Batch b, uint32_t x, int env_offset,
+                           hipStream_t s) {
+  const int blocks = (b.N + 255) / 256;
+  hipLaunchKernelGGL(env_seed_kernel, dim3(blocks), dim3(256), 0, s, b, x,
+                     env_offset);
+  return hipGetLastError();
+}
+
 }  // namespace xh

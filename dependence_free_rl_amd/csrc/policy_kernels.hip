@@ -510,8 +510,7 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
   uint32_t *srng = reinterpret_cast<uint32_t *>(sitem + G * 4);  // [G]
   int *sleft = reinterpret_cast<int *>(srng + G);                // [G]
   int *sflag = sleft + G;                                        // [1]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
-            h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31;
   const int o2t = w % S::NOT;
   const int rt0 = S::NOT >= 4 ? 0 : w / S::NOT;
   const bool fwd_active = (w / S::NOT) * S::FJ < 2;
@@ -521,11 +520,15 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
     if (w == 0) {  // construct: bins at capacity, one item (2 draws)
       const int e = lane / B, bin = lane % B, env = g * G + e;
       uint32_t x = mstd_jump(a.x0, (uint64_t)env * a.stream_stride);
-      const bool first = canonical(x) < a.env.p_a;
+      bool first = false;
+      if (!a.init_items) first = canonical(x) < a.env.p_a;
       for (int d = 0; d < D; ++d) sbins[e * S::BD + bin * D + d] = kCapacity;
       if (bin == 0) {
         for (int d = 0; d < 4; ++d)
-          sitem[e * 4 + d] = d < D ? (first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+          sitem[e * 4 + d] =
+              d >= D ? 0
+              : a.init_items ? a.init_items[env * D + d]
+              : (first ? a.env.item_a[d] : a.env.item_b[d]);
         srng[e] = x;
         sleft[e] = a.episodes;
         a.total[env] = 0.0;
@@ -607,6 +610,8 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
             srng[e] = x;
             if (done) sleft[e] -= 1;
             reward += done ? 0.0 : 1.0;
+            if (a.trace && g == 0 && e == 0 && nsteps < a.trace_cap)
+              a.trace[nsteps] = choice;
             ++nsteps;
           }
         }
@@ -621,6 +626,9 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
       const int env = g * G + lane / B;
       a.total[env] = reward;
       a.steps[env] = nsteps;
+      a.rng_out[env] = srng[lane / B];
+      for (int d = 0; d < D; ++d)
+        a.final_items[env * D + d] = sitem[(lane / B) * 4 + d];
     }
   }
 }

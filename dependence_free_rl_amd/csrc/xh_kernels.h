@@ -110,8 +110,13 @@ struct EvalArgs {
   uint32_t x0;
   uint64_t stream_stride;
   long max_steps;     // safety bound per env
+  const int *init_items;  // [n_envs][D] device, or nullptr: construct
   double *total;      // [n_envs] summed rewards
   long *steps;        // [n_envs] env steps taken
+  int *final_items;   // [n_envs][D]
+  uint32_t *rng_out;  // [n_envs]
+  int *trace;         // env 0's actions [trace_cap] or nullptr
+  long trace_cap;
 };
 
 // Launchers (return hipError_t of the launch). `variant` selects the
@@ -119,6 +124,8 @@ struct EvalArgs {
 bool policy_shape_supported(int B, int D, int H1, int H2);
 hipError_t launch_env_init(const EnvDesc &env, Batch b, uint32_t x0,
                            int env_offset, int n_global, hipStream_t s);
+hipError_t launch_env_seed(Batch b, uint32_t x, int env_offset,
+                           hipStream_t s);
 hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                hipStream_t s);
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,

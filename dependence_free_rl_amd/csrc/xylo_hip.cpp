@@ -256,6 +256,11 @@ void *buffer_ptr(const xh_trainer *t, int which) {
   return nullptr;
 }
 
+int copy_ok(hipError_t e) {
+  return e == hipSuccess ? XH_OK
+                         : fail(XH_ERR_HIP, "copy: %s", hipGetErrorString(e));
+}
+
 int refresh_value_transpose(xh_trainer *t) {
   return timed(t, "value", [&]() {
     return xh::launch_transpose(t->vp + t->vl.oW1(), t->vw1t, t->vl.V1,
@@ -742,55 +747,85 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
   });
 }
 
-int xh_trainer_evaluate(xh_trainer *t, int n_envs, int episodes,
-                        uint32_t rng_state, int argmax_probs, double *totals,
-                        long *steps) {
+int xh_trainer_evaluate(xh_trainer *t, xh_eval *e) {
   return guard([&]() -> int {
-    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    if (!t || !e) return fail(XH_ERR_INVALID, "null trainer / eval");
     const int G = t->cfg.bins <= 64 ? 64 / t->cfg.bins : 0;
+    const int n = e->n_envs, D = t->cfg.dims;
     if (G == 0)
       return fail(XH_ERR_INVALID, "evaluate: bins %d > 64 not supported",
                   t->cfg.bins);
-    if (n_envs <= 0 || n_envs % G || episodes < 0)
+    if (n <= 0 || n % G || e->episodes < 0 || e->trace_cap < 0)
       return fail(XH_ERR_INVALID, "evaluate: n_envs %d (multiple of %d), "
-                  "episodes %d", n_envs, G, episodes);
+                  "episodes %d", n, G, e->episodes);
+    if (e->init_items)
+      for (long i = 0; i < (long)n * D; ++i)
+        if (e->init_items[i] != t->env.item_a[i % D] &&
+            e->init_items[i] != t->env.item_b[i % D])
+          return fail(XH_ERR_INVALID, "evaluate: init_items[%ld] = %d is not "
+                      "an item of the table", i, e->init_items[i]);
     HIPCHK(hipSetDevice(t->ctx->device));
     hipStream_t s = t->ctx->stream;
-    double *dtot = nullptr;
-    long *dsteps = nullptr;
-    HIPCHK(hipMallocAsync((void **)&dtot, sizeof(double) * n_envs, s));
-    HIPCHK(hipMallocAsync((void **)&dsteps, sizeof(long) * n_envs, s));
+    // one scratch block: totals | steps | rng | init items | final items | trace
+    const size_t o_steps = sizeof(double) * n, o_rng = o_steps + 8 * (size_t)n,
+                 o_init = o_rng + 4 * (size_t)n,
+                 o_fin = o_init + 4 * (size_t)n * D,
+                 o_trace = o_fin + 4 * (size_t)n * D,
+                 bytes = o_trace + 4 * (size_t)(e->trace ? e->trace_cap : 0);
+    char *scratch = nullptr;
+    HIPCHK(hipMallocAsync((void **)&scratch, bytes, s));
     xh::EvalArgs a{};
     a.env = t->env;
     a.params = t->pp;
-    a.n_envs = n_envs;
-    a.episodes = episodes;
-    a.argmax_probs = argmax_probs ? 1 : 0;
-    uint32_t x0 = rng_state % 2147483647u;
+    a.n_envs = n;
+    a.episodes = e->episodes;
+    a.argmax_probs = e->argmax_probs ? 1 : 0;
+    const uint32_t x0 = e->rng_state % 2147483647u;
     a.x0 = x0 ? x0 : 1u;
     a.stream_stride = 1ull << 26;
     // an episode lasts at most B * capacity * D + 1 steps (every step puts
     // at least one unit into some bin)
-    a.max_steps = (long)(episodes + 1) * (t->cfg.bins * 8 * t->cfg.dims + 2);
-    a.total = dtot;
-    a.steps = dsteps;
-    int st = timed(t, "evaluate", [&]() {
-      return xh::launch_eval_argmax(a, t->cfg.policy_h1, t->cfg.policy_h2, s);
-    });
-    if (st == XH_OK && totals)
-      st = hipMemcpyAsync(totals, dtot, sizeof(double) * n_envs,
-                          hipMemcpyDeviceToHost, s) == hipSuccess
-               ? XH_OK
-               : fail(XH_ERR_HIP, "evaluate: copy");
-    if (st == XH_OK && steps)
-      st = hipMemcpyAsync(steps, dsteps, sizeof(long) * n_envs,
-                          hipMemcpyDeviceToHost, s) == hipSuccess
-               ? XH_OK
-               : fail(XH_ERR_HIP, "evaluate: copy");
-    (void)hipFreeAsync(dtot, s);
-    (void)hipFreeAsync(dsteps, s);
+    a.max_steps = (long)(e->episodes + 1) * (t->cfg.bins * 8 * D + 2);
+    a.total = (double *)scratch;
+    a.steps = (long *)(scratch + o_steps);
+    a.rng_out = (uint32_t *)(scratch + o_rng);
+    a.final_items = (int *)(scratch + o_fin);
+    a.trace = e->trace ? (int *)(scratch + o_trace) : nullptr;
+    a.trace_cap = e->trace ? e->trace_cap : 0;
+    int st = XH_OK;
+    if (e->init_items) {
+      a.init_items = (const int *)(scratch + o_init);
+      st = copy_ok(hipMemcpyAsync(scratch + o_init, e->init_items,
+                                  4 * (size_t)n * D, hipMemcpyHostToDevice, s));
+    }
+    if (st == XH_OK)
+      st = timed(t, "evaluate", [&]() {
+        return xh::launch_eval_argmax(a, t->cfg.policy_h1, t->cfg.policy_h2, s);
+      });
+    auto out = [&](void *host, size_t off, size_t nb) {
+      if (st == XH_OK && host)
+        st = copy_ok(hipMemcpyAsync(host, scratch + off, nb,
+                                    hipMemcpyDeviceToHost, s));
+    };
+    out(e->totals, 0, sizeof(double) * n);
+    out(e->steps, o_steps, 8 * (size_t)n);
+    out(e->rng_out, o_rng, 4 * (size_t)n);
+    out(e->final_items, o_fin, 4 * (size_t)n * D);
+    out(e->trace, o_trace, 4 * (size_t)a.trace_cap);
+    (void)hipFreeAsync(scratch, s);
     HIPCHK(hipStreamSynchronize(s));
     return st;
+  });
+}
+
+int xh_trainer_seed_streams(xh_trainer *t, uint32_t x) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    x %= 2147483647u;
+    HIPCHK(hipSetDevice(t->ctx->device));
+    HIPCHK(xh::launch_env_seed(t->batch(), x ? x : 1u, t->cfg.env_offset,
+                               t->ctx->stream));
+    return XH_OK;
   });
 }
 

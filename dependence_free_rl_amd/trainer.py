@@ -202,15 +202,38 @@ class Trainer:
         a = np.ascontiguousarray(arr, dt).reshape(shape)
         check(_lib.lib.xh_trainer_set_buffer(self.h, which, _ptr(a), a.nbytes))
 
-    def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False):
-        """Argmax evaluation (deep_agent.cc / the drivers' periodic eval):
-        returns (total reward per env, env steps per env)."""
-        tot = np.zeros(n_envs, np.float64)
-        steps = np.zeros(n_envs, np.int64)
-        check(_lib.lib.xh_trainer_evaluate(self.h, n_envs, episodes, rng_state,
-                                           1 if argmax_probs else 0, _ptr(tot),
-                                           _ptr(steps)))
-        return tot, steps
+    def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False,
+                 init_items=None, trace_cap=0):
+        """Argmax evaluation (deep_agent.cc / the drivers' periodic eval).
+        Returns a dict: totals, steps, final_items, rng (per env) and, with
+        trace_cap > 0, env 0's first trace_cap actions."""
+        D = self.D
+        out = {"totals": np.zeros(n_envs, np.float64),
+               "steps": np.zeros(n_envs, np.int64),
+               "final_items": np.zeros((n_envs, D), np.int32),
+               "rng": np.zeros(n_envs, np.uint32),
+               "trace": np.zeros(max(trace_cap, 1), np.int32)}
+        e = _lib.Eval()
+        e.n_envs, e.episodes = n_envs, episodes
+        e.argmax_probs, e.rng_state = 1 if argmax_probs else 0, rng_state
+        if init_items is not None:
+            init = np.ascontiguousarray(init_items, np.int32).reshape(n_envs, D)
+            e.init_items = init.ctypes.data
+        e.final_items = out["final_items"].ctypes.data
+        e.rng_out = out["rng"].ctypes.data
+        e.totals = out["totals"].ctypes.data
+        e.steps = out["steps"].ctypes.data
+        if trace_cap > 0:
+            e.trace, e.trace_cap = out["trace"].ctypes.data, trace_cap
+        check(_lib.lib.xh_trainer_evaluate(self.h, C.byref(e)))
+        if trace_cap <= 0:
+            del out["trace"]
+        return out
+
+    def seed_streams(self, x):
+        """Re-base the env streams on global engine state x (reference order:
+        env g steps from x advanced 4*T*g draws)."""
+        check(_lib.lib.xh_trainer_seed_streams(self.h, x))
 
     # ------------------------------------------------------------ timing --
     def set_timing(self, on):

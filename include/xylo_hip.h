@@ -130,16 +130,43 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
                           size_t bytes);
 
 /* Deterministic evaluation (policy_gradient_deterministic_policy,
- * policy_gradient.h:356-373; deep_agent.cc:25-41; the drivers' 100-episode
- * eval, ppo_training.cc:67-81) with the trainer's current policy: n_envs
- * independent envs (multiple of 64/bins) each play `episodes` whole episodes,
- * argmax action (over the softmax output if argmax_probs, else the logits).
+ * policy_gradient.h:356-373; agent::play_one_episode, rl.h:351-354; the
+ * drivers' 100-episode eval, ppo_training.cc:67-81; deep_agent.cc:25-41)
+ * with the trainer's current policy.  n_envs independent envs (a multiple of
+ * 64/bins) each play `episodes` whole episodes taking the argmax action (over
+ * the softmax output if argmax_probs, else over the raw logits).
+ *
  * Env e's minstd_rand0 stream starts at rng_state advanced by e * 2^26 draws,
- * so env 0 reproduces a single-env reference run seeded at rng_state.
- * totals/steps (host, n_envs each, may be NULL): summed rewards, env steps. */
-int xh_trainer_evaluate(xh_trainer *t, int n_envs, int episodes,
-                        uint32_t rng_state, int argmax_probs, double *totals,
-                        long *steps);
+ * so env 0 reproduces a single-env reference run whose global engine is at
+ * rng_state.  With init_items == NULL every env is first constructed
+ * (bins at capacity + get_item = 2 draws, bin_packing.h:50-52); otherwise env
+ * e starts with bins at capacity and item init_items[e*dims ...] (an env that
+ * was constructed or reset earlier) and draws nothing before its first step.
+ * Outputs (host arrays, each may be NULL): totals/steps per env (summed
+ * rewards, env steps), final_items (item after the last reset), rng_out (the
+ * stream state after the last draw), trace (env 0's actions, the first
+ * trace_cap of them). */
+typedef struct xh_eval {
+  int n_envs;
+  int episodes;
+  int argmax_probs;
+  uint32_t rng_state;
+  const int32_t *init_items; /* [n_envs][dims] or NULL */
+  int32_t *final_items;      /* [n_envs][dims] or NULL */
+  uint32_t *rng_out;         /* [n_envs] or NULL */
+  double *totals;            /* [n_envs] or NULL */
+  long *steps;               /* [n_envs] or NULL */
+  int32_t *trace;            /* [trace_cap] or NULL */
+  long trace_cap;
+} xh_eval;
+int xh_trainer_evaluate(xh_trainer *t, xh_eval *e);
+
+/* Re-base the per-env engine streams on a global minstd_rand0 state x: the
+ * next rollout steps env g (global index) from x advanced by 4*T*g draws, i.e.
+ * the reference order in which worker 0 plays its T steps, then worker 1, ...
+ * (ppo_training.cc:53-62 run sequentially, 4 draws per step).  After that
+ * rollout the global engine is at x advanced by 4*T*num_envs_global. */
+int xh_trainer_seed_streams(xh_trainer *t, uint32_t x);
 
 /* Kernel timing with HIP events on the trainer's stream (off by default). */
 int xh_trainer_set_timing(xh_trainer *t, int on);

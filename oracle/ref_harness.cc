@@ -434,13 +434,17 @@ int mode_deep(std::map<std::string, std::string> &a) {
   recorder rec(a["out"]);
   uint32_t seed = iarg(a, "seed", 1);
   long episodes = iarg(a, "episodes", 1000);
+  // main=1: exactly deep_agent.cc's order -- the engine is seeded before the
+  // model is built (its He init draws), no logits section, no reseed.
+  const bool as_main = iarg(a, "main", 0) != 0;
+  if (as_main) xylo::default_generator().seed(seed);
   xylo::model m;
   build_perbin(m, 4, {128, 64}, head_none);
   xeno::sys::mmap f = xeno::sys::mmap<float>(a["weights"]);
   xylo::vector_view v = xylo::borrow_vector(f.span());
   m.set_parameters(v);
   rec.f32("params", to_std(m.parameters()));
-
+  if (!as_main) {
   // Logits for a few fixed observations (bins, item) -> golden Dense forward.
   std::vector<float> obs_all, logits_all;
   xylo::default_generator().seed(seed + 1000);
@@ -463,8 +467,8 @@ int mode_deep(std::map<std::string, std::string> &a) {
   }
   rec.f32("obs", obs_all, {64, 32});
   rec.f32("logits", logits_all, {64, 8});
-
   xylo::default_generator().seed(seed);
+  }
   uint32_t x0 = engine_state();
   xylo::policy_gradient_deterministic_policy<bp::action, bp::observation> pol(
       m);
@@ -481,6 +485,61 @@ int mode_deep(std::map<std::string, std::string> &a) {
   rec.i32("episode_len", lens);
   std::fprintf(stderr, "deep: %ld episodes total reward %g\n", episodes,
                total);
+  return 0;
+}
+
+// ------------------------------------------------------ mode: driver -------
+// The model + env construction prologue of ppo_training.cc:9-43 (algo=ppo)
+// or ac_training.cc (algo=ac) after seeding the engine: initial parameters
+// and the engine state once the workers' envs exist.  Pins the drop-in
+// layer's initialisation against the reference's (tests/test_compat.py).
+int mode_driver(std::map<std::string, std::string> &a) {
+  recorder rec(a["out"]);
+  xylo::default_generator().seed(iarg(a, "seed", 1));
+  const bool ac = a["algo"] == "ac";
+  xylo::model pol, val;
+  build_perbin(pol, 4, ac ? std::vector<int>{64, 32} : std::vector<int>{128, 64},
+               ac ? head_softmax_xent : head_softmax);
+  build_full(val, 4 * bp::num_bins, {64, 32}, 1, head_none);
+  const uint32_t x_models = engine_state();
+  std::vector<bp::environment> envs;
+  const long n = iarg(a, "workers", ac ? 16 : 8);
+  envs.reserve(n);
+  for (long i = 0; i < n; ++i) envs.emplace_back();
+  rec.f32("policy_init", to_std(pol.parameters()));
+  rec.f32("value_init", to_std(val.parameters()));
+  rec.u32("x_models", {x_models});
+  rec.u32("x_envs", {engine_state()});
+  std::vector<int32_t> items;
+  for (auto &e : envs) {
+    bp::observation o = e.view(0);
+    items.push_back(o.item.first);
+    items.push_back(o.item.second);
+  }
+  rec.i32("items", items);
+  return 0;
+}
+
+// ------------------------------------------------------ mode: random -------
+// random_agent.cc's loop (rounds x 100 episodes of xylo::random_policy),
+// seeded: per-round average reward.
+int mode_random(std::map<std::string, std::string> &a) {
+  recorder rec(a["out"]);
+  xylo::default_generator().seed(iarg(a, "seed", 1));
+  const long rounds = iarg(a, "rounds", 3), episodes = iarg(a, "episodes", 100);
+  std::vector<float> avg;
+  for (long r = 0; r < rounds; ++r) {
+    xylo::random_policy<bp::num_bins, bp::observation> policy;
+    bp::environment env;
+    xylo::replay_buffer<bp::action, bp::observation> rb;
+    bp::agent agent(policy, env, rb);
+    for (long i = 0; i < episodes; ++i) agent.play_one_episode();
+    auto exp = rb.sample_td();
+    avg.push_back(xylo::total_rewards<bp::action, bp::observation>(exp) /
+                  double(episodes));
+    rb.forget();
+  }
+  rec.f32("round_avg", avg);
   return 0;
 }
 
@@ -727,6 +786,8 @@ int main(int argc, char **argv) {
   if (mode == "rng") return mode_rng(a);
   if (mode == "envcheck") return mode_envcheck(a);
   if (mode == "deep") return mode_deep(a);
+  if (mode == "driver") return mode_driver(a);
+  if (mode == "random") return mode_random(a);
   if (mode == "learn") return mode_learn(a, false);
   if (mode == "bench") return mode_learn(a, true);
   std::fprintf(stderr, "unknown mode %s\n", mode.c_str());

@@ -76,6 +76,16 @@ FIXTURES = {
     # BASELINE config 5 shape (3-D, 128 bins, [128,128], actor-critic)
     "ac_b128d3": ("learn", ["algo=ac", "B=128", "D=3", "widths=128,128",
                             "N=2", "T=8", "iters=2", "seed=13"]),
+    # deep_agent.cc's first round as its main runs it (engine seeded 1
+    # before the model's He init draws; 10000 episodes)
+    "deep_w20_main": ("deep", ["seed=1", "episodes=10000", "main=1",
+                               "weights=%s/apps/bin_packing/weights.20" % REF]),
+    # ppo_training.cc / ac_training.cc prologue seeded: initial parameters
+    # and engine state after the workers' envs (pins include/xylo_compat)
+    "driver_ppo_s7": ("driver", ["algo=ppo", "seed=7"]),
+    "driver_ac_s7": ("driver", ["algo=ac", "seed=7"]),
+    # random_agent.cc's loop seeded: 3 rounds x 100 episodes
+    "random_s5": ("random", ["seed=5", "rounds=3", "episodes=100"]),
     # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])
     "pg_b8d1": ("learn", ["algo=pg", "B=8", "D=1", "widths=32", "N=1",
                           "episodes=4", "iters=3", "seed=17"]),

