@@ -12,11 +12,11 @@ LIB_PATH = os.path.join(HERE, "libxylo_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "xylo_hip.h")
 
 XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)
-XH_PPO, XH_AC = 0, 1
+XH_PPO, XH_AC, XH_KLPPO = 0, 1, 2
 XH_POLICY, XH_VALUE = 0, 1
 (BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
  BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
- BUF_LOGITS, BUF_PROBS, BUF_V_STATE0) = range(15)
+ BUF_LOGITS, BUF_PROBS, BUF_V_STATE0, BUF_QOLD, BUF_KL) = range(17)
 
 
 class XhError(RuntimeError):
@@ -33,7 +33,8 @@ class Config(C.Structure):
         ("lr_policy", C.c_float), ("lr_value", C.c_float),
         ("wd_policy", C.c_float), ("wd_value", C.c_float), ("gamma", C.c_float),
         ("lambda_", C.c_float), ("clip_eps", C.c_float),
-        ("rng_state", C.c_uint32)]
+        ("rng_state", C.c_uint32), ("kl_beta", C.c_float),
+        ("kl_target", C.c_float)]
 
 
 class Eval(C.Structure):

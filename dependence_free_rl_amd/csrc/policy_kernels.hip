@@ -283,6 +283,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
       const float p = ex / sum;
       if (a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
       if (a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
+      if (a.qold_out) a.qold_out[((size_t)t * N + env) * B + bin] = p;
 
       uint32_t x = a.b.rng[env];
       int choice;
@@ -634,7 +635,12 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
 }
 
 // ============================================================ train epoch ==
-template <class S>
+// KL = true: kl_ppo_learner's epoch (policy_gradient.h:310-335) -- every row
+// of the state matrix: transitions, then the open trajectories' end rows
+// (slot T, q of step T-1), then the terminal end rows E_t of end_list (the
+// overflowed view, rl.h:336-343); end rows have A = 0 and the previous
+// action's distribution (policy_gradient.h:178).
+template <class S, bool KL>
 __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
@@ -644,7 +650,11 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
             h = lane >> 5;
   const int N = a.b.N, T = a.b.T;
   const int gpt = N / S::G;  // groups per step
-  const int ngroups = T * gpt;
+  const int gmain = T * gpt;
+  const int n_end = KL ? *a.n_end : 0;
+  const int ngroups = KL ? gmain + gpt + (n_end + S::G - 1) / S::G : gmain;
+  const float beta = KL ? *a.beta : 0.0f;
+  double kl_acc = 0.0;
   float *H1img = lds + S::L_H1;
   float *DAimg = lds + S::L_DA2;
 
@@ -670,21 +680,66 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
 
   // prefetched per-group inputs: two rows per lane + this lane's env record
   RowRaw<S> cur, nxt;
-  int c_cur = 0, c_nxt = 0;
+  int c_cur = 0, c_nxt = 0, v_cur = 1, v_nxt = 1;
   float po_cur = 1.0f, po_nxt = 1.0f, A_cur = 0.0f, A_nxt = 0.0f;
-  auto fetch = [&](int g, RowRaw<S> &rr, int &c, float &po, float &A) {
-    const int t = g / gpt, e0 = (g - t * gpt) * S::G;
-    fetch_rows<S>(a.b, t, e0, rr);
-    const size_t ti = (size_t)t * N + e0 + lane / B;
-    c = a.b.action[ti];
-    po = a.b.pold[ti];
-    A = a.adv[ti];
+  float q_cur = 1.0f, q_nxt = 1.0f;
+  auto fetch = [&](int g, RowRaw<S> &rr, int &c, float &po, float &A, float &q,
+                   int &valid) {
+    if constexpr (!KL) {
+      const int t = g / gpt, e0 = (g - t * gpt) * S::G;
+      fetch_rows<S>(a.b, t, e0, rr);
+      const size_t ti = (size_t)t * N + e0 + lane / B;
+      c = a.b.action[ti];
+      po = a.b.pold[ti];
+      A = a.adv[ti];
+    } else {
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int r = rt * 32 + lr, el = r / B, bin = r % B;
+        int t, e, kind, ok = 1;
+        if (g < gmain) {
+          t = g / gpt;
+          e = (g - t * gpt) * S::G + el;
+          kind = 0;
+        } else if (g < gmain + gpt) {
+          t = T;
+          e = (g - gmain) * S::G + el;
+          kind = 1;
+          ok = a.b.done[(size_t)(T - 1) * N + e] == 0;
+        } else {
+          const int j = (g - gmain - gpt) * S::G + el;
+          kind = 2;
+          ok = j < n_end;
+          const int te = ok ? a.end_list[j] : 0;
+          t = te / N;
+          e = te - t * N;
+        }
+        const size_t env = (size_t)t * N + e;
+        const int8_t *bp = a.b.bins + env * S::BD + bin * S::D;
+        const int8_t *ip = a.b.items + env * 4;
+        const bool sub = kind == 2 && a.b.action[env] == bin;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          rr.iv[rt][d] = ip[d];
+          rr.bv[rt][d] = bp[d] - (sub ? ip[d] : 0);
+        }
+        if (rt == h) {  // this lane's own row (= lane) of the loss head
+          c = kind == 0 ? a.b.action[env] : 0;
+          A = kind == 0 ? a.adv[env] : 0.0f;
+          po = 1.0f;
+          const size_t qrow = kind == 1 ? (size_t)(T - 1) * N + e : env;
+          q = a.qold[qrow * B + bin];
+          valid = ok;
+        }
+      }
+    }
   };
-  if ((int)blockIdx.x < ngroups) fetch(blockIdx.x, cur, c_cur, po_cur, A_cur);
+  if ((int)blockIdx.x < ngroups)
+    fetch(blockIdx.x, cur, c_cur, po_cur, A_cur, q_cur, v_cur);
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int gn = g + gridDim.x;
-    if (gn < ngroups) fetch(gn, nxt, c_nxt, po_nxt, A_nxt);
+    if (gn < ngroups) fetch(gn, nxt, c_nxt, po_nxt, A_nxt, q_nxt, v_nxt);
     f32x16 pre[S::FJ];
     f32x16 h1own[2];
     {
@@ -737,7 +792,17 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
       const float p = ex / seg_sum<B>(ex);
       const int c = c_cur;
       const float A = A_cur;
-      if (a.ablate & 8) {
+      if constexpr (KL) {
+        // kl_regulated_loss: softmax_gradient_log + beta (p - q), applied as
+        // a probability-space gradient through softmax_layer::backward
+        // (nn.h:393-417): gz_j = p_j (g_j - sum_k p_k g_k)
+        float gp = p * A + beta * (p - q_cur);
+        if (bin == c) gp -= A;
+        const float sg = seg_sum<B>(p * gp);
+        gz = v_cur ? p * (gp - sg) : 0.0f;
+        if (w == 0 && v_cur)
+          kl_acc += (double)q_cur * log((double)q_cur / (double)p);
+      } else if (a.ablate & 8) {
         gz = z * 1e-3f;
       } else if (a.algo == kPPO) {
         // clipped_gradient (rl.h:54-74) then softmax_layer::backward
@@ -840,6 +905,15 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
     c_cur = c_nxt;
     po_cur = po_nxt;
     A_cur = A_nxt;
+    q_cur = q_nxt;
+    v_cur = v_nxt;
+  }
+  if constexpr (KL) {
+    if (w == 0) {
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) kl_acc += __shfl_xor(kl_acc, o, kWave);
+      if (lane == 0) a.kl_part[blockIdx.x] = kl_acc;
+    }
   }
 
   // ---------------------------------------------------- slab write-out ----
@@ -1398,22 +1472,34 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
     using S = PShape<XB, XD, XH1, XH2>;                                      \
     static bool attr = false;                                                \
     if (!attr) {                                                             \
-      if constexpr (S::HG == 1)                                              \
-        (void)hipFuncSetAttribute((const void *)policy_train_kernel<S>,      \
+      if constexpr (S::HG == 1) {                                            \
+        (void)hipFuncSetAttribute((const void *)policy_train_kernel<S, false>,\
                                   hipFuncAttributeMaxDynamicSharedMemorySize,\
                                   (int)train_lds<S>());                      \
+        (void)hipFuncSetAttribute((const void *)policy_train_kernel<S, true>,\
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                  (int)train_lds<S>());                      \
+      }                                                                      \
       if constexpr (S::NIT == 4 && S::NOT == 4)                              \
         (void)hipFuncSetAttribute((const void *)policy_train8_kernel<S>,     \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,\
                                   (int)train_lds<S>());                      \
       attr = true;                                                           \
     }                                                                        \
+    if (a.algo == kKLPPO) {                                                  \
+      if constexpr (S::HG == 1)                                              \
+        hipLaunchKernelGGL((policy_train_kernel<S, true>), dim3(grid),       \
+                           dim3(256), train_lds<S>(), s, a);                 \
+      else                                                                   \
+        return hipErrorInvalidValue;                                         \
+      return hipGetLastError();                                              \
+    }                                                                        \
     if constexpr (S::NIT == 4 && S::NOT == 4 && (!XH_TRAIN4 || S::HG > 1))  \
       hipLaunchKernelGGL(policy_train8_kernel<S>, dim3(grid), dim3(512),     \
                          train_lds<S>(), s, a);                              \
     else if constexpr (S::HG == 1)                                           \
-      hipLaunchKernelGGL(policy_train_kernel<S>, dim3(grid), dim3(256),      \
-                         train_lds<S>(), s, a);                              \
+      hipLaunchKernelGGL((policy_train_kernel<S, false>), dim3(grid),        \
+                         dim3(256), train_lds<S>(), s, a);                   \
     return hipGetLastError();                                                \
   }
   XH_POLICY_SHAPES(X)

@@ -6,7 +6,7 @@
 
 namespace xh {
 
-enum Algo { kPPO = 0, kAC = 1 };
+enum Algo { kPPO = 0, kAC = 1, kKLPPO = 2 };
 
 // Flat parameter offsets of the per-bin policy, in the reference layout
 // model::parameters() (nn.h:499-508): conv1d_1(F0->H1), relu,
@@ -65,6 +65,7 @@ struct RolloutArgs {
   const int32_t *forced;  // optional [T][N] actions (teacher forcing)
   float *logits_out;      // optional [N][B] (debug / parity)
   float *probs_out;       // optional [N][B]
+  float *qold_out;        // KL-PPO: [T][N][B] the sampled distribution
 };
 
 struct PolicyTrainArgs {
@@ -78,6 +79,23 @@ struct PolicyTrainArgs {
   int slab_stride;
   int ablate;        // diagnostics only (XH_ABLATE): bit0 skip dW2, bit1 skip
                      // dH1/dW1, bit2 skip layer-2 fwd, bit3 skip softmax/loss
+  // KL-PPO (kl_regulated_loss): every row of the learner's state matrix,
+  // i.e. the T*N transitions, the open trajectories' end rows (slot T) and
+  // the terminal end rows E_t listed in end_list.
+  const float *qold;     // [T][N][B] old distributions
+  const float *beta;     // device scalar (adapted between epochs)
+  const int *end_list;   // [n_end] t*N + env of terminal transitions
+  const int *n_end;      // device scalar
+  double *kl_part;       // [gridDim.x] sum over rows of KL(q || p)
+};
+
+// End-row bookkeeping for KL-PPO (one 1024-thread workgroup).
+struct EndListArgs {
+  const uint8_t *done;   // [T][N]
+  int N, T;
+  int *end_list;         // [T*N] env-major, t ascending
+  int *n_end;            // scalar
+  int *n_open;           // scalar: envs whose last step is not terminal
 };
 
 struct ValueArgs {
@@ -126,6 +144,14 @@ hipError_t launch_env_init(const EnvDesc &env, Batch b, uint32_t x0,
                            int env_offset, int n_global, hipStream_t s);
 hipError_t launch_env_seed(Batch b, uint32_t x, int env_offset,
                            hipStream_t s);
+hipError_t launch_end_list(const EndListArgs &a, hipStream_t s);
+// beta <- adapt(beta, mean KL) (policy_gradient.h:68-80); kl_sum[0] = the
+// (all-reduced) KL sum, rows[0] the (all-reduced) row count.
+hipError_t launch_kl_reduce(const double *kl_part, int nparts, const int *n_end,
+                            const int *n_open, double rows_main,
+                            double *kl_sum, hipStream_t s);
+hipError_t launch_kl_beta_update(const double *kl_sum, float *beta,
+                                 float d_targ, float *log, hipStream_t s);
 hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                hipStream_t s);
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,

@@ -128,6 +128,10 @@ struct xh_trainer {
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
   float *logits = nullptr, *probs = nullptr;
+  // KL-PPO state
+  float *qold = nullptr, *beta = nullptr, *kl_log = nullptr;
+  int *end_list = nullptr, *n_end = nullptr, *n_open = nullptr;
+  double *kl_part = nullptr, *kl_sum = nullptr;
   uint32_t jump_mul = 1;
   int rgrid = 0;
   bool need_shift = false;
@@ -213,6 +217,16 @@ int allreduce(xh_trainer *t, float *buf, int n) {
   });
 }
 
+int allreduce_d(xh_trainer *t, double *buf, int n) {
+  if (t->ctx->world <= 1) return XH_OK;
+  hipStream_t s = t->ctx->stream;
+  return timed(t, "allreduce", [&]() -> hipError_t {
+    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum,
+                                   t->ctx->comm, s);
+    return r == ncclSuccess ? hipSuccess : hipErrorUnknown;
+  });
+}
+
 size_t buffer_bytes(const xh_trainer *t, int which) {
   const size_t N = t->N(), T = t->T();
   switch (which) {
@@ -231,6 +245,8 @@ size_t buffer_bytes(const xh_trainer *t, int which) {
     case XH_BUF_POLICY_GRADS: return (size_t)t->cfg.epochs * t->np * 4;
     case XH_BUF_LOGITS: return N * t->cfg.bins * 4;
     case XH_BUF_PROBS: return N * t->cfg.bins * 4;
+    case XH_BUF_QOLD: return t->qold ? T * N * t->cfg.bins * 4 : 0;
+    case XH_BUF_KL: return t->kl_log ? (size_t)t->cfg.epochs * 12 : 0;
   }
   return 0;
 }
@@ -243,6 +259,8 @@ void *buffer_ptr(const xh_trainer *t, int which) {
     case XH_BUF_POLD: return t->pold;
     case XH_BUF_DONE: return t->done;
     case XH_BUF_RNG: return t->rng;
+    case XH_BUF_QOLD: return t->qold;
+    case XH_BUF_KL: return t->kl_log;
     case XH_BUF_V_STATE: return t->v_state;
     case XH_BUF_V_STATE0: return t->v_state0;
     case XH_BUF_V_TERM: return t->v_term;
@@ -284,6 +302,7 @@ int do_rollout(xh_trainer *t) {
   a.jump_mul = t->jump_mul;
   a.params = t->pp;
   a.forced = t->use_forced ? t->forced : nullptr;
+  a.qold_out = t->qold;  // KL-PPO only (nullptr otherwise)
   for (int step = 0; step < (int)T; ++step) {
     a.t = step;
     const bool last = step == (int)T - 1;
@@ -349,6 +368,17 @@ int do_learn(xh_trainer *t) {
     const char *ab = std::getenv("XH_ABLATE");  // diagnostics only
     pa.ablate = ab ? std::atoi(ab) : 0;
   }
+  const bool kl = c.algo == XH_KLPPO;
+  if (kl) {
+    pa.qold = t->qold;
+    pa.beta = t->beta;
+    pa.end_list = t->end_list;
+    pa.n_end = t->n_end;
+    pa.kl_part = t->kl_part;
+    xh::EndListArgs ea{t->done, (int)t->N(), (int)t->T(), t->end_list,
+                       t->n_end, t->n_open};
+    CHK(timed(t, "kl", [&]() { return xh::launch_end_list(ea, s); }));
+  }
   for (int e = 0; e < c.epochs; ++e) {
     float *g = t->pgrads + (size_t)e * t->np;
     CHK(timed(t, "policy_train", [&]() {
@@ -360,6 +390,18 @@ int do_learn(xh_trainer *t) {
                                     t->np, g, s);
     }));
     CHK(allreduce(t, g, t->np));
+    if (kl) {  // mean KL over the job's rows -> beta for the next epoch
+      CHK(timed(t, "kl", [&]() {
+        return xh::launch_kl_reduce(t->kl_part, t->pslab_n, t->n_end,
+                                    t->n_open, (double)t->T() * t->N(),
+                                    t->kl_sum, s);
+      }));
+      CHK(allreduce_d(t, t->kl_sum, 2));
+      CHK(timed(t, "kl", [&]() {
+        return xh::launch_kl_beta_update(t->kl_sum, t->beta, c.kl_target,
+                                         t->kl_log + 3 * e, s);
+      }));
+    }
     CHK(timed(t, "reduce_sgd", [&]() {
       return xh::launch_sgd(t->pp, g, t->np, c.lr_policy, c.wd_policy, s);
     }));
@@ -475,27 +517,33 @@ void xh_config_default(xh_config *c, int algo, int bins, int dims, int num_envs,
   c->bins = bins;
   c->dims = dims;
   c->steps = steps;
-  c->epochs = algo == XH_PPO ? 4 : 1;
+  c->epochs = algo == XH_AC ? 1 : 4;
   c->policy_h1 = 128;
-  c->policy_h2 = algo == XH_PPO ? 64 : 32;
+  c->policy_h2 = algo == XH_AC ? 32 : 64;
   if (algo == XH_AC) c->policy_h1 = 64;
   c->value_h1 = 64;
   c->value_h2 = 32;
   // ppo_training.cc:17,26 / ac_training.cc:17,26
-  c->lr_policy = algo == XH_PPO ? 1e-4f : 1e-5f;
-  c->lr_value = algo == XH_PPO ? 1e-5f : 1e-4f;
+  c->lr_policy = algo == XH_AC ? 1e-5f : 1e-4f;
+  c->lr_value = algo == XH_AC ? 1e-4f : 1e-5f;
+  if (algo == XH_KLPPO) c->wd_policy = 1e-5f;  // ppo2_training.cc:20
   c->gamma = 0.99f;
   c->lambda = 0.95f;
   c->clip_eps = 0.2f;
   c->rng_state = 1;
+  c->kl_beta = 1.0f;
+  c->kl_target = 1e-9f;
 }
 
 int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
   return guard([&]() -> int {
     if (!ctx || !cfg || !out) return fail(XH_ERR_INVALID, "null arg");
     const xh_config &c = *cfg;
-    if (c.algo != XH_PPO && c.algo != XH_AC)
+    if (c.algo != XH_PPO && c.algo != XH_AC && c.algo != XH_KLPPO)
       return fail(XH_ERR_INVALID, "algo %d", c.algo);
+    if (c.algo == XH_KLPPO && c.bins > 64)
+      return fail(XH_ERR_INVALID, "KL-PPO: bins %d > 64 not supported",
+                  c.bins);
     if (!xh::policy_shape_supported(c.bins, c.dims, c.policy_h1, c.policy_h2))
       return fail(XH_ERR_INVALID,
                   "unsupported policy shape B=%d D=%d widths=[%d,%d]", c.bins,
@@ -578,6 +626,24 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->vgrad, (size_t)t->nv * 4);
     A(&t->logits, N * c.bins * 4);
     A(&t->probs, N * c.bins * 4);
+    if (c.algo == XH_KLPPO) {
+      A(&t->qold, T * N * c.bins * 4);
+      A(&t->beta, 4);
+      A(&t->kl_log, (size_t)c.epochs * 3 * 4);
+      A(&t->end_list, T * N * 4);
+      A(&t->n_end, 4);
+      A(&t->n_open, 4);
+      A(&t->kl_part, (size_t)t->pslab_n * 8);
+      A(&t->kl_sum, 2 * 8);
+    }
+    if (st != XH_OK) {
+      std::string keep = g_err;
+      xh_trainer_destroy(t);
+      g_err = keep;
+      return st;
+    }
+    if (st == XH_OK && t->beta)
+      st = copy_ok(hipMemcpy(t->beta, &c.kl_beta, 4, hipMemcpyHostToDevice));
     if (st != XH_OK) {
       std::string keep = g_err;
       xh_trainer_destroy(t);

@@ -18,12 +18,13 @@ import numpy as np
 
 from . import _lib
 from ._lib import (BUF_ACTION, BUF_ADV, BUF_BINS, BUF_DONE, BUF_ITEMS,
-                   BUF_LOGITS, BUF_POLD, BUF_POLICY_GRADS, BUF_PROBS, BUF_RNG,
-                   BUF_TARGETS, BUF_V_STATE, BUF_V_STATE0, BUF_V_TERM,
-                   BUF_VALUE_GRAD, XH_AC, XH_POLICY, XH_PPO, XH_VALUE, check)
+                   BUF_KL, BUF_LOGITS, BUF_POLD, BUF_POLICY_GRADS, BUF_PROBS,
+                   BUF_QOLD, BUF_RNG, BUF_TARGETS, BUF_V_STATE, BUF_V_STATE0,
+                   BUF_V_TERM, BUF_VALUE_GRAD, XH_AC, XH_KLPPO, XH_POLICY,
+                   XH_PPO, XH_VALUE, check)
 
 POLICY, VALUE = XH_POLICY, XH_VALUE
-ALGOS = {"ppo": XH_PPO, "ac": XH_AC}
+ALGOS = {"ppo": XH_PPO, "ac": XH_AC, "klppo": XH_KLPPO}
 
 
 def _ptr(a):
@@ -105,11 +106,12 @@ def init_value(bins, dims, v1=64, v2=32, seed=1):
 
 class Trainer:
     """xh_trainer: N vectorised bin-packing envs + per-bin policy + value net +
-    PPO (ppo_learner) or actor-critic (actor_critic_learner) learner."""
+    PPO (ppo_learner), KL-PPO (kl_ppo_learner) or actor-critic
+    (actor_critic_learner) learner."""
 
     def __init__(self, ctx, algo="ppo", bins=64, dims=2, num_envs=4096, steps=4,
                  widths=(128, 128), value_widths=(64, 32), epochs=None,
-                 lr_policy=None, lr_value=None, wd_policy=0.0, wd_value=0.0,
+                 lr_policy=None, lr_value=None, wd_policy=None, wd_value=None,
                  gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
                  num_envs_global=None, env_offset=0):
         cfg = _lib.Config()
@@ -125,7 +127,10 @@ class Trainer:
             cfg.lr_policy = lr_policy
         if lr_value is not None:
             cfg.lr_value = lr_value
-        cfg.wd_policy, cfg.wd_value = wd_policy, wd_value
+        if wd_policy is not None:
+            cfg.wd_policy = wd_policy
+        if wd_value is not None:
+            cfg.wd_value = wd_value
         cfg.gamma, cfg.lambda_, cfg.clip_eps = gamma, lam, clip_eps
         cfg.rng_state = rng_state
         self.cfg = cfg
@@ -189,6 +194,8 @@ class Trainer:
             BUF_POLICY_GRADS: (np.float32, (self.epochs, self.np_)),
             BUF_LOGITS: (np.float32, (N, B)),
             BUF_PROBS: (np.float32, (N, B)),
+            BUF_QOLD: (np.float32, (T, N, B)),
+            BUF_KL: (np.float32, (self.epochs, 3)),
         }[which]
 
     def buffer(self, which):

@@ -326,20 +326,21 @@ class session {
     const policy_shape ps = parse_policy(*learner_.action_model);
     const auto vs = parse_value(*learner_.value_model);
     const bool ac = learner_.kind == xylo::learner_kind::actor_critic;
-    if (learner_.kind == xylo::learner_kind::kl_ppo)
-      throw xeno::error("xylo-hip: kl_ppo_learner is not on the device yet");
+    const bool klppo = learner_.kind == xylo::learner_kind::kl_ppo;
     const int want_head = int(ac ? xylo::layer_kind::softmax_xent
                                  : xylo::layer_kind::softmax);
     if (ps.head != want_head)
       throw xeno::error(ac ? "xylo-hip: ac_learner needs a "
                              "softmax_cross_entropy_layer head"
-                           : "xylo-hip: ppo_learner needs a softmax_layer head");
+                           : "xylo-hip: ppo_learner / kl_ppo_learner need a "
+                             "softmax_layer head");
     for (xylo::optimizer *o :
          {learner_.action_optimizer, learner_.value_optimizer})
       if (o->kind() != xylo::optimizer_kind::sgd)
         throw xeno::error("xylo-hip: only sgd_optimizer runs on the device");
     xh_config c;
-    xh_config_default(&c, ac ? XH_AC : XH_PPO, int(num_bins), 2, N, T_);
+    xh_config_default(&c, ac ? XH_AC : klppo ? XH_KLPPO : XH_PPO,
+                      int(num_bins), 2, N, T_);
     c.policy_h1 = ps.h1;
     c.policy_h2 = ps.h2;
     c.value_h1 = vs.first;
@@ -500,7 +501,9 @@ class session {
       std::ofstream j(std::string(p) + ".json");
       j << "{\"x0\": " << x_first_ << ", \"num_envs\": " << envs_.size()
         << ", \"steps\": " << T_ << ", \"learner_steps\": " << steps_
-        << ", \"algo\": \"" << (tr_->cfg.algo == XH_AC ? "ac" : "ppo")
+        << ", \"algo\": \""
+        << (tr_->cfg.algo == XH_AC ? "ac"
+                                   : tr_->cfg.algo == XH_KLPPO ? "klppo" : "ppo")
         << "\", \"h1\": " << tr_->cfg.policy_h1 << ", \"h2\": "
         << tr_->cfg.policy_h2 << ", \"v1\": " << tr_->cfg.value_h1
         << ", \"v2\": " << tr_->cfg.value_h2 << ", \"lr_policy\": "

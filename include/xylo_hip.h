@@ -57,16 +57,20 @@ int xh_ctx_synchronize(xh_ctx *ctx);
 int xh_ctx_allreduce_host(xh_ctx *ctx, float *data, size_t n);
 
 /* ------------------------------------------------------------ trainer --- */
-enum { XH_PPO = 0, XH_AC = 1 };
+/* XH_KLPPO: kl_ppo_learner (policy_gradient.h:310-335, ppo2_training.cc):
+ * PPO's k = 4 full-batch epochs with kl_regulated_loss and an adaptive beta
+ * that carries over from one learn() to the next.  Per-bin shapes with
+ * bins <= 64. */
+enum { XH_PPO = 0, XH_AC = 1, XH_KLPPO = 2 };
 
 typedef struct {
-  int algo;            /* XH_PPO (ppo_learner) | XH_AC (actor_critic_learner) */
+  int algo;            /* XH_PPO | XH_AC (actor_critic_learner) | XH_KLPPO */
   int num_envs;        /* envs on this rank (multiple of 64/bins)            */
   int num_envs_global; /* envs in the whole job (reference-order RNG streams) */
   int env_offset;      /* global index of this rank's first env              */
   int bins, dims;      /* B (bin_packing.h:12 num_bins), D (2 in the ref)    */
   int steps;           /* T: env steps per env per iteration (play_steps(T)) */
-  int epochs;          /* PPO k (policy_gradient.h:300), 1 for AC            */
+  int epochs;          /* PPO / KL-PPO k (policy_gradient.h:300), 1 for AC  */
   int policy_h1, policy_h2; /* per-bin conv1d_1 widths                       */
   int value_h1, value_h2;   /* value full_layer widths (64, 32)              */
   float lr_policy, lr_value, wd_policy, wd_value;
@@ -74,6 +78,8 @@ typedef struct {
   float lambda;        /* 0.95 (policy_gradient.h:286) */
   float clip_eps;      /* 0.2  (rl.h:56) */
   uint32_t rng_state;  /* minstd_rand0 state before the envs are constructed */
+  float kl_beta;       /* KL-PPO initial beta (1, policy_gradient.h:332)     */
+  float kl_target;     /* KL-PPO d_targ (1e-9, policy_gradient.h:333)        */
 } xh_config;
 
 /* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */
@@ -122,6 +128,9 @@ enum {
   XH_BUF_LOGITS = 12,  /* f32   [N][B]  logits of the last rollout step      */
   XH_BUF_PROBS = 13,   /* f32   [N][B]  probabilities of the last step       */
   XH_BUF_V_STATE0 = 14,/* f32   [T+1][N] V(S_t) before the value step        */
+  XH_BUF_QOLD = 15,    /* f32   [T][N][B] KL-PPO: sampled distributions      */
+  XH_BUF_KL = 16,      /* f32   [epochs][3] KL-PPO: beta used, mean KL, new
+                                  beta of the last learn()                   */
   XH_BUF_COUNT
 };
 size_t xh_trainer_buffer_bytes(const xh_trainer *t, int which);

@@ -404,6 +404,7 @@ struct or_trainer {
   float *pp, *vp; /* params */
   size_t np, nv;
   float lr_pi, lr_v, wd_pi, wd_v, gamma, lambda;
+  float beta, d_targ; /* kl_ppo_learner (policy_gradient.h:332-333) */
   uint32_t x;
   /* workers */
   int32_t *bins, *item; /* N*B*D, N*D */
@@ -477,6 +478,8 @@ or_trainer *or_trainer_create(int algo, const or_env_cfg *env, int N, int T,
   t->wd_v = wd_v;
   t->gamma = gamma;
   t->lambda = 0.95f; /* policy_gradient.h:286 */
+  t->beta = 1.0f;
+  t->d_targ = 1e-9f;
   t->x = x0;
   const int BD = env->B * env->D;
   t->bins = (int32_t *)malloc(sizeof(int32_t) * (size_t)N * BD);
@@ -661,13 +664,24 @@ typedef struct {
   const float *pold;
   const float *adv;
   int ppo;
+  /* KL-PPO: old distributions [rows][cols], adaptive beta, target KL */
+  const float *qold;
+  float *beta;
+  float d_targ;
+  double d_avg; /* out: mean KL(q || p) of the call */
 } pl_ctx;
 /* PPO: surrogate_loss -> clipped_gradient (policy_gradient.h:28-38,
  * rl.h:54-74).  AC / PG: policy_loss -> softmax_gradient_log
  * (policy_gradient.h:16-26, rl.h:45-52). */
+static void loss_kl(pl_ctx *c, const float *out, int rows, int cols,
+                    float *g);
 static void loss_policy(void *ctx, const float *out, int rows, int cols,
                         float *g) {
-  const pl_ctx *c = (const pl_ctx *)ctx;
+  pl_ctx *c = (pl_ctx *)ctx;
+  if (c->qold) {
+    loss_kl(c, out, rows, cols, g);
+    return;
+  }
   for (int r = 0; r < rows; ++r) {
     const float *p = out + (size_t)r * cols;
     float *o = g + (size_t)r * cols;
@@ -692,6 +706,42 @@ static void loss_policy(void *ctx, const float *out, int rows, int cols,
   }
 }
 
+/* kl_regulated_loss (policy_gradient.h:41-85): softmax_gradient_log rows
+ * (rl.h:45-52) + beta * softmax_cross_entropy_loss_grad(q, p) = beta (p - q)
+ * (nn.h:584-586), then the mean KL(q || p) over all rows (kl_divergence,
+ * :41-46) adapts beta for the next call: halve below d_targ / 1.5, double
+ * above 1.5 d_targ, clamp to [1e-25, 0.1].  The gradient uses the beta from
+ * before the update. */
+static void loss_kl(pl_ctx *c, const float *out, int rows, int cols,
+                    float *g) {
+  const float beta = *c->beta;
+  double dsum = 0.0;
+  for (int r = 0; r < rows; ++r) {
+    const float *p = out + (size_t)r * cols;
+    const float *q = c->qold + (size_t)r * cols;
+    float *o = g + (size_t)r * cols;
+    const float A = c->adv[r];
+    for (int j = 0; j < cols; ++j) o[j] = p[j] * A;
+    o[c->choice[r]] -= A;
+    double d = 0.0;
+    for (int j = 0; j < cols; ++j) {
+      o[j] += beta * (p[j] - q[j]);
+      d += (double)q[j] * log((double)q[j] / (double)p[j]);
+    }
+    dsum += d;
+  }
+  const float d_avg = (float)(dsum / rows);
+  c->d_avg = d_avg;
+  float b = beta;
+  if (fabsf(d_avg) < c->d_targ / 1.5f)
+    b /= 2;
+  else if (fabsf(d_avg) > c->d_targ * 1.5f)
+    b *= 2;
+  if (b < 1e-25f) b = 1e-25f;
+  if (b > 0.1f) b = 0.1f;
+  *c->beta = b;
+}
+
 void or_trainer_learn(or_trainer *t) {
   const or_env_cfg *c = &t->env;
   const int B = c->B, D = c->D, len = 2 * D * B;
@@ -706,6 +756,7 @@ void or_trainer_learn(or_trainer *t) {
   int32_t *renv = (int32_t *)malloc(sizeof(int32_t) * rows);
   int32_t *rstep = (int32_t *)malloc(sizeof(int32_t) * rows);
   int32_t *rend = (int32_t *)malloc(sizeof(int32_t) * rows);
+  float *qrows = (float *)malloc(sizeof(float) * (size_t)rows * B);
   /* state_matrix: transitions + one end row per trajectory, end-row action =
    * copy of the previous one (policy_gradient.h:168-180) */
   int r = 0;
@@ -716,6 +767,7 @@ void or_trainer_learn(or_trainer *t) {
       or_obs(c, tr->start.bins, tr->start.item, sm + (size_t)r * len);
       choice[r] = tr->choice;
       pold[r] = tr->distrib[tr->choice];
+      memcpy(qrows + (size_t)r * B, tr->distrib, sizeof(float) * B);
       renv[r] = tr->start.env;
       rstep[r] = tr->start.step;
       rend[r] = 0;
@@ -726,6 +778,8 @@ void or_trainer_learn(or_trainer *t) {
       or_obs(c, bk->end.bins, bk->end.item, sm + (size_t)r * len);
       choice[r] = choice[r - 1];
       pold[r] = pold[r - 1];
+      memcpy(qrows + (size_t)r * B, qrows + (size_t)(r - 1) * B,
+             sizeof(float) * B);
       renv[r] = bk->end.env;
       rstep[r] = bk->end.step;
       rend[r] = 1;
@@ -759,7 +813,7 @@ void or_trainer_learn(or_trainer *t) {
     }
     float avg = total / (float)t->nlist;
     for (int i = 0; i < rows; ++i) adv[i] = adv[i] - avg;
-    pl_ctx pc = {choice, pold, adv, 0};
+    pl_ctx pc = {choice, pold, adv, 0, NULL, NULL, 0, 0};
     or_model_grad(&t->pol, t->pp, sm, rows, len, loss_policy, &pc, pgrad);
     buf_append(&t->buf[OR_BUF_POLICY_GRADS], pgrad, t->np, sizeof(float));
     or_sgd(t->pp, pgrad, t->np, t->lr_pi, t->wd_pi);
@@ -830,11 +884,22 @@ void or_trainer_learn(or_trainer *t) {
 
     /* optimize_action: PPO k=4 surrogate steps (policy_gradient.h:297-307),
      * AC one policy_loss step (:187-194) */
-    const int epochs = t->algo == OR_PPO ? 4 : 1;
-    pl_ctx pc = {choice, pold, adv, t->algo == OR_PPO};
+    const int epochs = t->algo == OR_AC ? 1 : 4;
+    pl_ctx pc = {choice, pold, adv, t->algo == OR_PPO, NULL, NULL, 0, 0};
+    if (t->algo == OR_KLPPO) {
+      pc.qold = qrows;
+      pc.beta = &t->beta;
+      pc.d_targ = t->d_targ;
+    }
+    buf_clear(&t->buf[OR_BUF_KL]);
     for (int e = 0; e < epochs; ++e) {
+      const float beta_used = t->beta;
       or_model_grad(&t->pol, t->pp, sm, rows, len, loss_policy, &pc, pgrad);
       buf_append(&t->buf[OR_BUF_POLICY_GRADS], pgrad, t->np, sizeof(float));
+      if (t->algo == OR_KLPPO) {
+        const float kl[3] = {beta_used, (float)pc.d_avg, t->beta};
+        buf_append(&t->buf[OR_BUF_KL], kl, 3, sizeof(float));
+      }
       or_sgd(t->pp, pgrad, t->np, t->lr_pi, t->wd_pi);
     }
   }
@@ -844,6 +909,7 @@ void or_trainer_learn(or_trainer *t) {
   free(sm);
   free(choice);
   free(pold);
+  free(qrows);
   free(renv);
   free(rstep);
   free(rend);
@@ -879,7 +945,7 @@ void or_policy_grad_rows(const or_model *m, const float *params, const float *x,
                          float *grad) {
   int *ch = (int *)malloc(sizeof(int) * (rows > 0 ? rows : 1));
   for (int r = 0; r < rows; ++r) ch[r] = choice[r];
-  pl_ctx pc = {ch, pold, adv, algo == OR_PPO};
+  pl_ctx pc = {ch, pold, adv, algo == OR_PPO, NULL, NULL, 0, 0};
   or_model_grad(m, params, x, rows, xcols, loss_policy, &pc, grad);
   free(ch);
 }

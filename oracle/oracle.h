@@ -80,7 +80,7 @@ void or_model_grad(const or_model *m, const float *params, const float *x,
 void or_sgd(float *params, const float *grad, size_t n, float lr, float wd);
 
 /* --------------------------------------------------------------- learner -- */
-enum { OR_PPO = 0, OR_AC = 1, OR_PG = 2 };
+enum { OR_PPO = 0, OR_AC = 1, OR_PG = 2, OR_KLPPO = 3 };
 
 typedef struct or_trainer or_trainer;
 
@@ -119,6 +119,8 @@ enum {
   OR_BUF_FINAL_ITEM,    /* int32  [N][D]                                   */
   OR_BUF_ROW_CHOICE,    /* int32  [rows]  action of the row                */
   OR_BUF_ROW_POLD,      /* float  [rows]  distrib[choice] of the row       */
+  OR_BUF_KL,            /* float  [epochs][3] KL-PPO: beta used, mean KL,
+                                              beta after                   */
   OR_BUF_COUNT
 };
 /* Returns a pointer to the buffer and its element count. */

@@ -13,11 +13,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 
 OR_FULL, OR_POINT, OR_RELU, OR_SOFTMAX, OR_SOFTMAX_XENT = range(5)
-OR_PPO, OR_AC, OR_PG = range(3)
+OR_PPO, OR_AC, OR_PG, OR_KLPPO = range(4)
 (BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE, BUF_STEP_PCHOICE,
  BUF_ROWS, BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_VALUES, BUF_TARGETS,
  BUF_VALUE_GRAD, BUF_ADVANTAGES, BUF_POLICY_GRADS, BUF_FINAL_BINS,
- BUF_FINAL_ITEM, BUF_ROW_CHOICE, BUF_ROW_POLD) = range(18)
+ BUF_FINAL_ITEM, BUF_ROW_CHOICE, BUF_ROW_POLD, BUF_KL) = range(19)
 _INT_BUFS = {BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE,
              BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_FINAL_BINS,
              BUF_FINAL_ITEM, BUF_ROW_CHOICE}

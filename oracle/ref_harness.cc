@@ -545,7 +545,7 @@ int mode_random(std::map<std::string, std::string> &a) {
 
 // ------------------------------------------------------- mode: learn -------
 struct learn_cfg {
-  std::string algo;  // ppo | ac | pg
+  std::string algo;  // ppo | klppo | ac | pg
   int N, T, iters;
   std::vector<int> widths, vwidths;
   float lr_pi, lr_v, wd_pi, wd_v, gamma;
@@ -568,7 +568,7 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     build_full(pol, B * f0, c.widths, B, head_softmax_xent);
   else
     build_perbin(pol, f0, c.widths,
-                 c.algo == "ppo" ? head_softmax : head_softmax_xent);
+                 c.algo == "ac" ? head_softmax_xent : head_softmax);
   if (!pg) build_full(val, B * f0, c.vwidths, 1, head_none);
   recording_sgd opt_pi(pol, c.lr_pi, c.wd_pi), opt_v(val, c.lr_v, c.wd_v);
   opt_pi.record = opt_v.record = rec != nullptr;
@@ -595,6 +595,9 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
   if (c.algo == "ppo")
     ac = std::make_unique<xylo::ppo_learner<A, S>>(rb, pol, opt_pi, val, opt_v,
                                                    c.gamma);
+  else if (c.algo == "klppo")  // ppo2_training.cc
+    ac = std::make_unique<xylo::kl_ppo_learner<A, S>>(rb, pol, opt_pi, val,
+                                                      opt_v, c.gamma);
   else if (c.algo == "ac")
     ac = std::make_unique<xylo::actor_critic_learner<A, S>>(
         rb, pol, opt_pi, val, opt_v, c.gamma);

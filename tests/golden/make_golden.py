@@ -70,6 +70,11 @@ FIXTURES = {
     # BASELINE config 3/4 shape (2-D, 64 bins, [128,128])
     "ppo_b64d2": ("learn", ["algo=ppo", "B=64", "D=2", "widths=128,128",
                             "N=4", "T=4", "iters=2", "seed=11"]),
+    # ppo2_training.cc: KL-regulated PPO, conv 4->128->64->1 + softmax,
+    # policy sgd(1e-4, wd 1e-5), 16 workers x 8 steps; beta carries over
+    "klppo_b8d2": ("learn", ["algo=klppo", "B=8", "D=2", "widths=128,64",
+                             "N=16", "T=8", "iters=4", "wd_pi=1e-5",
+                             "seed=21"]),
     # ac_training.cc shapes: conv 4->64->32->1 + softmax-xent, 16x8
     "ac_b8d2": ("learn", ["algo=ac", "B=8", "D=2", "widths=64,32", "N=16",
                           "T=8", "iters=4", "seed=3"]),
@@ -84,6 +89,7 @@ FIXTURES = {
     # and engine state after the workers' envs (pins include/xylo_compat)
     "driver_ppo_s7": ("driver", ["algo=ppo", "seed=7"]),
     "driver_ac_s7": ("driver", ["algo=ac", "seed=7"]),
+    "driver_ppo2_s7": ("driver", ["algo=ppo", "seed=7", "workers=16"]),
     # random_agent.cc's loop seeded: 3 rounds x 100 episodes
     "random_s5": ("random", ["seed=5", "rounds=3", "episodes=100"]),
     # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])

@@ -14,6 +14,9 @@ def trainer_from_golden(ctx, name, **kw):
     kv = meta(g)
     B, D, N, T = int(kv["B"]), int(kv["D"]), int(kv["N"]), int(kv.get("T", 4))
     widths = tuple(int(w) for w in kv["widths"].split(","))
+    if "wd_pi" in kv:
+        kw.setdefault("wd_policy", float(kv["wd_pi"]))
+    kw.setdefault("wd_policy", 0.0)
     tr = Trainer(ctx, algo=kv["algo"], bins=B, dims=D, num_envs=N, steps=T,
                  widths=widths, rng_state=int(g["x0"][0]), **kw)
     tr.set_params(POLICY, g["init_policy"])

@@ -2,7 +2,7 @@
 include/xylo_compat by `make compat`) running on the GPU, checked against the
 CPU oracle and the reference's golden vectors.
 
-ppo_training / ac_training: seeded (XYLO_SEED), stopped after the second
+ppo_training / ac_training / ppo2_training (KL-PPO): seeded (XYLO_SEED), stopped after the second
 learner.step() (XYLO_HIP_MAX_STEPS), parameters dumped per step
 (XYLO_HIP_DUMP).  The first iteration (8 / 16 workers' windows, value step,
 GAE, surrogate epochs) must match the oracle within 1e-4, and the step-0
@@ -23,9 +23,11 @@ from conftest import assert_close, golden
 pytestmark = pytest.mark.gpu
 
 DRIVERS = {
-    # algo, workers, T, widths, lr_pi, lr_v, head
-    "ppo_training": ("ppo", 8, 4, (128, 64), 1e-4, 1e-5),
-    "ac_training": ("ac", 16, 8, (64, 32), 1e-5, 1e-4),
+    # algo, workers, T, widths, lr_pi, lr_v, wd_pi, prologue fixture
+    "ppo_training": ("ppo", 8, 4, (128, 64), 1e-4, 1e-5, 0.0, "driver_ppo_s7"),
+    "ac_training": ("ac", 16, 8, (64, 32), 1e-5, 1e-4, 0.0, "driver_ac_s7"),
+    "ppo2_training": ("klppo", 16, 8, (128, 64), 1e-4, 1e-5, 1e-5,
+                      "driver_ppo2_s7"),
 }
 
 
@@ -38,7 +40,7 @@ def _need(name):
 def test_reference_driver_on_gpu(tmp_path, name):
     from oracle import pyoracle as po
     _need(name)
-    algo, N, T, widths, lr_pi, lr_v = DRIVERS[name]
+    algo, N, T, widths, lr_pi, lr_v, wd_pi, fixture = DRIVERS[name]
     prefix = str(tmp_path / "run")
     env = dict(os.environ, XYLO_SEED="7", XYLO_HIP_MAX_STEPS="2",
                XYLO_HIP_DUMP=prefix)
@@ -47,7 +49,7 @@ def test_reference_driver_on_gpu(tmp_path, name):
     assert got and got[0][0] == 0, text[-2000:]
     meta = json.load(open(prefix + ".json"))
     assert (meta["num_envs"], meta["steps"]) == (N, T)
-    g = golden("driver_%s_s7" % algo)
+    g = golden(fixture)
     pol0 = np.fromfile(prefix + ".policy.0.bin", np.float32)
     val0 = np.fromfile(prefix + ".value.0.bin", np.float32)
     np.testing.assert_array_equal(pol0, g["policy_init"])
@@ -55,12 +57,12 @@ def test_reference_driver_on_gpu(tmp_path, name):
     assert meta["x0"] == int(g["x_envs"][0])
 
     # iteration 0 on the oracle, envs constructed from the same engine state
-    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    head = po.OR_SOFTMAX_XENT if algo == "ac" else po.OR_SOFTMAX
     pm = po.perbin_model(4, list(widths), head)
     vm = po.full_model(32, [64, 32], 1)
-    orc = po.Trainer(po.OR_PPO if algo == "ppo" else po.OR_AC, 8, 2, N, T, pm,
-                     pol0, vm, val0, lr_pi=lr_pi, lr_v=lr_v,
-                     x0=int(g["x_models"][0]))
+    code = {"ppo": po.OR_PPO, "ac": po.OR_AC, "klppo": po.OR_KLPPO}[algo]
+    orc = po.Trainer(code, 8, 2, N, T, pm, pol0, vm, val0, lr_pi=lr_pi,
+                     lr_v=lr_v, wd_pi=wd_pi, x0=int(g["x_models"][0]))
     orc.rollout()
     orc.learn()
     pol1 = np.fromfile(prefix + ".policy.1.bin", np.float32)

@@ -25,7 +25,8 @@ def ctx():
     c.close()
 
 
-ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3"]
+ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3",
+             "klppo_b8d2"]
 
 
 @pytest.mark.parametrize("name", ENV_CASES)
@@ -97,7 +98,7 @@ def test_rollout_sampling_matches_reference(ctx, name):
 
 
 @pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2",
-                                  "ac_b128d3"])
+                                  "ac_b128d3", "klppo_b8d2"])
 def test_learn_matches_reference(ctx, name):
     """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
     value gradient and updated parameters vs the reference learner."""
@@ -210,3 +211,32 @@ def test_evaluate_from_given_items(ctx):
         x, item = int(r["rng"][0]), list(r["final_items"][0])
     assert tot == whole["totals"][0] and n == whole["steps"][0]
     assert x == whole["rng"][0]
+
+
+def test_klppo_beta_and_old_distributions(ctx):
+    """kl_ppo_learner specifics: the rollout keeps each step's whole sampled
+    distribution (action.distrib, rl.h:27-30), and beta adapts per epoch
+    from the mean KL over ALL rows (end rows included) as the oracle's
+    restatement of kl_regulated_loss does (policy_gradient.h:41-85)."""
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd.trainer import BUF_KL, BUF_QOLD
+    tr, g, kv = trainer_from_golden(ctx, "klppo_b8d2")
+    N, T, B = tr.N, tr.T, tr.B
+    from test_oracle_golden import models_for
+    pol, val = models_for(kv)
+    orc = po.Trainer(po.OR_KLPPO, B, 2, N, T, pol, g["init_policy"], val,
+                     g["init_value"], wd_pi=1e-5, x0=int(g["x0"][0]))
+    for it in range(int(kv["iters"])):
+        p = "it%d_" % it
+        tr.set_forced_actions(step_major(g[p + "step_choice"], N, T))
+        tr.rollout()
+        assert_close(tr.buffer(BUF_QOLD),
+                     step_major(g[p + "step_distrib"], N, T), what="q_old")
+        tr.learn()
+        orc.rollout(forced=g[p + "step_choice"])
+        orc.learn()
+        okl = orc.buf(po.BUF_KL).reshape(-1, 3)
+        gkl = tr.buffer(BUF_KL)
+        np.testing.assert_array_equal(gkl[:, 0], okl[:, 0])   # beta used
+        np.testing.assert_array_equal(gkl[:, 2], okl[:, 2])   # beta after
+        assert_close(gkl[:, 1], okl[:, 1], what="mean KL")

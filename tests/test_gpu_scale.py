@@ -19,12 +19,14 @@ def ctx():
 
 def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     from oracle import pyoracle as po
-    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    head = po.OR_SOFTMAX_XENT if algo == "ac" else po.OR_SOFTMAX
     pol = po.perbin_model(2 * D, list(widths), head)
     val = po.full_model(B * 2 * D, [64, 32], 1)
-    return po.Trainer(po.OR_PPO if algo == "ppo" else po.OR_AC, B, D, N, T, pol,
-                      pp, val, vp, lr_pi=1e-4 if algo == "ppo" else 1e-5,
-                      lr_v=1e-5 if algo == "ppo" else 1e-4, x0=x0)
+    code = {"ppo": po.OR_PPO, "ac": po.OR_AC, "klppo": po.OR_KLPPO}[algo]
+    return po.Trainer(code, B, D, N, T, pol, pp, val, vp,
+                      lr_pi=1e-5 if algo == "ac" else 1e-4,
+                      lr_v=1e-4 if algo == "ac" else 1e-5,
+                      wd_pi=1e-5 if algo == "klppo" else 0.0, x0=x0)
 
 
 @pytest.mark.parametrize("algo,B,D,widths,N,T", [
@@ -32,6 +34,7 @@ def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     ("ppo", 32, 1, (64, 64), 64, 4),     # config 2 shape
     ("ac", 16, 2, (64, 64), 64, 8),
     ("ac", 128, 3, (128, 128), 8, 8),    # config 5 shape
+    ("klppo", 64, 2, (128, 128), 16, 4),  # KL-PPO at the config-3 shape
 ])
 def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
     from oracle import pyoracle as po

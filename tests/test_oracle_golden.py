@@ -23,7 +23,7 @@ def models_for(kv):
     if algo == "pg":
         pol = po.full_model(B * 2 * D, widths, B, po.OR_SOFTMAX_XENT)
         return pol, None
-    head = po.OR_SOFTMAX if algo == "ppo" else po.OR_SOFTMAX_XENT
+    head = po.OR_SOFTMAX_XENT if algo == "ac" else po.OR_SOFTMAX
     pol = po.perbin_model(2 * D, widths, head)
     val = po.full_model(B * 2 * D, [64, 32], 1)
     return pol, val
@@ -103,7 +103,9 @@ def test_weights20_logits_and_argmax_episodes():
 
 
 # ------------------------------------------------------------- learners ----
-LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1"]
+LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1",
+         "klppo_b8d2"]
+ALGO = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG, "klppo": po.OR_KLPPO}
 
 
 def run_oracle_against(name, forced=True):
@@ -111,13 +113,14 @@ def run_oracle_against(name, forced=True):
     kv = parse_meta(g)
     B, D, N = int(kv["B"]), int(kv["D"]), int(kv["N"])
     T = int(kv.get("T", 4))
-    algo = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG}[kv["algo"]]
+    algo = ALGO[kv["algo"]]
     pol, val = models_for(kv)
     lr_pi = 1e-5 if kv["algo"] == "ac" else 1e-4
     lr_v = 1e-4 if kv["algo"] == "ac" else 1e-5
     tr = po.Trainer(algo, B, D, N, T, pol, g["init_policy"], val,
                     g["init_value"] if val is not None else None, lr_pi=lr_pi,
-                    lr_v=lr_v, gamma=0.99, x0=int(g["x0"][0]),
+                    lr_v=lr_v, wd_pi=float(kv.get("wd_pi", 0.0)), gamma=0.99,
+                    x0=int(g["x0"][0]),
                     episodes=int(kv.get("episodes", 1)))
     iters = int(kv["iters"])
     worst = {}
@@ -163,7 +166,7 @@ def test_learner_matches_reference(name):
     print(name, {k: "%.2e" % v for k, v in worst.items()})
 
 
-@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "pg_b8d1"])
+@pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "pg_b8d1", "klppo_b8d2"])
 def test_free_running_sampling_matches_reference(name):
     """Without teacher forcing the oracle's own sampler reproduces the
     reference's actions (no probability near-ties in these fixtures)."""
