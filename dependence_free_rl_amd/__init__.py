@@ -2,8 +2,9 @@
 path for vectorised bin packing (drop-in for beehover/dependence_free_rl's
 xylo::rl / xylo::policy_gradient hot path).  See DESIGN.md."""
 from ._lib import XhError, lib  # noqa: F401  (fails loudly if not built)
-from .trainer import (ALGOS, POLICY, VALUE, Context, Trainer, init_policy,  # noqa: F401
-                      init_value, policy_param_count, value_param_count)
+from .trainer import (ALGOS, POLICY, VALUE, Context, Trainer,  # noqa: F401
+                      heuristic_evaluate, init_policy, init_value,
+                      policy_param_count, value_param_count)
 
 __all__ = ["Context", "Trainer", "POLICY", "VALUE", "init_policy", "init_value",
-           "XhError"]
+           "heuristic_evaluate", "XhError"]

@@ -13,6 +13,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "xylo_hip.h")
 
 XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)
 XH_PPO, XH_AC, XH_KLPPO = 0, 1, 2
+HEURISTICS = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
 XH_POLICY, XH_VALUE = 0, 1
 (BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
  BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
@@ -44,7 +45,7 @@ class Eval(C.Structure):
         ("rng_state", C.c_uint32), ("init_items", C.c_void_p),
         ("final_items", C.c_void_p), ("rng_out", C.c_void_p),
         ("totals", C.c_void_p), ("steps", C.c_void_p), ("trace", C.c_void_p),
-        ("trace_cap", C.c_long)]
+        ("trace_cap", C.c_long), ("elapsed_ms", C.c_double)]
 
 
 def _load():
@@ -57,6 +58,7 @@ def _load():
     sig = {
         "xh_last_error": (C.c_char_p, []),
         "xh_version": (C.c_char_p, []),
+        "xh_struct_size": (sz, [C.c_char_p]),
         "xh_comm_unique_id": (i, [vp]),
         "xh_ctx_create": (i, [i, i, i, vp, C.POINTER(vp)]),
         "xh_ctx_destroy": (i, [vp]),
@@ -77,6 +79,7 @@ def _load():
         "xh_trainer_set_buffer": (i, [vp, i, vp, sz]),
         "xh_trainer_evaluate": (i, [vp, C.POINTER(Eval)]),
         "xh_trainer_seed_streams": (i, [vp, C.c_uint32]),
+        "xh_heuristic_evaluate": (i, [vp, i, i, i, C.POINTER(Eval)]),
         "xh_trainer_set_timing": (i, [vp, i]),
         "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_long)]),
@@ -90,6 +93,11 @@ def _load():
 
 
 lib = _load()
+for _name, _mirror in (("xh_config", Config), ("xh_eval", Eval)):
+    if lib.xh_struct_size(_name.encode()) != C.sizeof(_mirror):
+        raise ImportError("ctypes mirror of %s is out of date (%d vs %d bytes)"
+                          % (_name, C.sizeof(_mirror),
+                             lib.xh_struct_size(_name.encode())))
 
 
 def check(status):

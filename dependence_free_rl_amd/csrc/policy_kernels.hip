@@ -291,33 +291,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
         choice = a.forced[(size_t)t * N + env];
         (void)canonical(x);  // the sampler's two engine draws
       } else {
-        // std::discrete_distribution (random.tcc:2654-2713): p -> double,
-        // normalise by the sum, partial sums, last = 1, lower_bound(u).
-        const double pd = (double)p;
-        const double sd = seg_sum_d<B>(pd);
-        double cp = seg_scan_d<B>(pd / sd, lane);
-        if (bin == B - 1) cp = 1.0;
-        const double u = canonical(x);
-        const unsigned long long below = __ballot(cp < u);
-        unsigned long long segmask = ~0ull;
-        if constexpr (B < 64) segmask = ((1ull << B) - 1ull) << seg0;
-        choice = __popcll(below & segmask);
-        // Near a cumulative boundary the tree-ordered sums could round
-        // differently from the sequential ones: recompute sequentially.
-        const float gap = (float)fabs(cp - u);
-        if (seg_min<B>(gap) < 1e-9f) {
-          double s2 = 0.0;
-          for (int k = 0; k < B; ++k) s2 += (double)wave_shfl(p, seg0 + k);
-          double acc = 0.0;
-          int c2 = B - 1;
-          for (int k = 0; k < B; ++k) {
-            const double qk = (double)wave_shfl(p, seg0 + k) / s2;
-            acc = k == 0 ? qk : acc + qk;
-            const double cpk = k == B - 1 ? 1.0 : acc;
-            if (!(cpk < u) && k < c2) c2 = k;
-          }
-          choice = c2;
-        }
+        choice = sample_discrete<B>(p, lane, canonical(x));
       }
       const float pold = wave_shfl(p, seg0 + choice);
 
@@ -574,19 +548,7 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
           const float ex = expf(v);
           v = ex / seg_sum<B>(ex);
         }
-        // std::ranges::max_element: first maximum (tensor.cc:464-466)
-        float bv = v;
-        int bi = bin;
-#pragma unroll
-        for (int o = 1; o < B; o <<= 1) {
-          const float ov = __shfl_xor(bv, o, kWave);
-          const int oi = __shfl_xor(bi, o, kWave);
-          if (ov > bv || (ov == bv && oi < bi)) {
-            bv = ov;
-            bi = oi;
-          }
-        }
-        const int choice = bi;
+        const int choice = seg_argmax_first<B>(v, bin);  // tensor.cc:464-466
         const bool active = sleft[e] > 0;
         int nb[D];
         int neg = 0;

@@ -107,4 +107,56 @@ __device__ __forceinline__ float seg_min(float v) {
   return v;
 }
 
+// std::discrete_distribution<size_t>(p[0..B)) sampled with canonical u
+// (libstdc++ random.tcc:2654-2713): p -> double, normalise by the sum,
+// partial sums, last = 1.0, lower_bound(u).  Lane = bin of a B-lane segment
+// (`lane` its wave lane).  The tree-ordered sums agree with the sequential
+// ones except within rounding of a boundary; there the segment recomputes
+// sequentially.  Returns the chosen bin (the same in every lane).
+template <int B>
+__device__ __forceinline__ int sample_discrete(float p, int lane, double u) {
+  const int bin = lane & (B - 1), seg0 = lane - bin;
+  const double pd = (double)p;
+  const double sd = seg_sum_d<B>(pd);
+  double cp = seg_scan_d<B>(pd / sd, lane);
+  if (bin == B - 1) cp = 1.0;
+  const unsigned long long below = __ballot(cp < u);
+  unsigned long long segmask = ~0ull;
+  if constexpr (B < 64) segmask = ((1ull << B) - 1ull) << seg0;
+  int choice = __popcll(below & segmask);
+  const float gap = (float)fabs(cp - u);
+  if (seg_min<B>(gap) < 1e-9f) {
+    double s2 = 0.0;
+    for (int k = 0; k < B; ++k) s2 += (double)__shfl(p, seg0 + k, kWave);
+    double acc = 0.0;
+    int c2 = B - 1;
+    for (int k = 0; k < B; ++k) {
+      const double qk = (double)__shfl(p, seg0 + k, kWave) / s2;
+      acc = k == 0 ? qk : acc + qk;
+      const double cpk = k == B - 1 ? 1.0 : acc;
+      if (!(cpk < u) && k < c2) c2 = k;
+    }
+    choice = c2;
+  }
+  return choice;
+}
+
+// First maximum of v over a B-lane segment (std::ranges::max_element,
+// tensor.cc:464-466): ties go to the lowest bin.
+template <int B>
+__device__ __forceinline__ int seg_argmax_first(float v, int bin) {
+  float bv = v;
+  int bi = bin;
+#pragma unroll
+  for (int o = 1; o < B; o <<= 1) {
+    const float ov = __shfl_xor(bv, o, kWave);
+    const int oi = __shfl_xor(bi, o, kWave);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  return bi;
+}
+
 }  // namespace xh

@@ -7,6 +7,8 @@
 namespace xh {
 
 enum Algo { kPPO = 0, kAC = 1, kKLPPO = 2 };
+enum Heuristic { kHeurRandom = 0, kHeurFirstfit = 1, kHeurBestfit = 2,
+                 kHeurMinwaste = 3 };
 
 // Flat parameter offsets of the per-bin policy, in the reference layout
 // model::parameters() (nn.h:499-508): conv1d_1(F0->H1), relu,
@@ -136,6 +138,26 @@ struct EvalArgs {
   int *trace;         // env 0's actions [trace_cap] or nullptr
   long trace_cap;
 };
+
+// Heuristic agents (heuristic_kernels.hip): same stream / output convention
+// as EvalArgs.
+struct HeuristicArgs {
+  EnvDesc env;
+  int n_envs;
+  int episodes;
+  uint32_t x0;
+  uint64_t stream_stride;
+  long max_steps;
+  const int *init_items;
+  double *total;
+  long *steps;
+  int *final_items;
+  uint32_t *rng_out;
+  int *trace;
+  long trace_cap;
+};
+bool heuristic_shape_supported(int B, int D);
+hipError_t launch_heuristic(const HeuristicArgs &a, int kind, hipStream_t s);
 
 // Launchers (return hipError_t of the launch). `variant` selects the
 // <B,D,H1,H2> instantiation; returns hipErrorInvalidValue when unsupported.

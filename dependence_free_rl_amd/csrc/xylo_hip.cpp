@@ -279,6 +279,109 @@ int copy_ok(hipError_t e) {
                          : fail(XH_ERR_HIP, "copy: %s", hipGetErrorString(e));
 }
 
+constexpr uint64_t kEvalStride = 1ull << 26;  // draws between env streams
+
+xh::EnvDesc make_env(int bins, int dims) {
+  static const int ia[3][3] = {{4, 0, 0}, {4, 2, 0}, {4, 2, 2}};
+  static const int ib[3][3] = {{1, 0, 0}, {1, 2, 0}, {1, 2, 1}};
+  xh::EnvDesc env{};
+  env.B = bins;
+  env.D = dims;
+  for (int d = 0; d < 3; ++d) {
+    env.item_a[d] = ia[dims - 1][d];
+    env.item_b[d] = ib[dims - 1][d];
+  }
+  env.p_a = 0.4;
+  return env;
+}
+
+struct EvalBuffers {
+  uint32_t x0;
+  long max_steps;
+  const int *init_items;
+  double *total;
+  long *steps;
+  uint32_t *rng_out;
+  int *final_items;
+  int *trace;
+  long trace_cap;
+};
+
+// Shared host side of the episode evaluators (xh_trainer_evaluate,
+// xh_heuristic_evaluate): one device scratch block for the per-env outputs,
+// the launch bracketed by HIP events (e->elapsed_ms), copies back, sync.
+template <class Launch>
+int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
+                Launch launch) {
+  const int n = e->n_envs, D = env.D;
+  if (n <= 0 || n % G || e->episodes < 0 || e->trace_cap < 0)
+    return fail(XH_ERR_INVALID, "evaluate: n_envs %d (multiple of %d), "
+                "episodes %d", n, G, e->episodes);
+  if (e->init_items)
+    for (long i = 0; i < (long)n * D; ++i)
+      if (e->init_items[i] != env.item_a[i % D] &&
+          e->init_items[i] != env.item_b[i % D])
+        return fail(XH_ERR_INVALID, "evaluate: init_items[%ld] = %d is not "
+                    "an item of the table", i, e->init_items[i]);
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t o_steps = sizeof(double) * n, o_rng = o_steps + 8 * (size_t)n,
+               o_init = o_rng + 4 * (size_t)n,
+               o_fin = o_init + 4 * (size_t)n * D,
+               o_trace = o_fin + 4 * (size_t)n * D,
+               bytes = o_trace + 4 * (size_t)(e->trace ? e->trace_cap : 0);
+  char *scratch = nullptr;
+  HIPCHK(hipMallocAsync((void **)&scratch, bytes, s));
+  EvalBuffers eb{};
+  const uint32_t x0 = e->rng_state % 2147483647u;
+  eb.x0 = x0 ? x0 : 1u;
+  // an episode lasts at most B * capacity * D + 1 steps (every step puts at
+  // least one unit into some bin)
+  eb.max_steps = (long)(e->episodes + 1) * (env.B * 8 * D + 2);
+  eb.total = (double *)scratch;
+  eb.steps = (long *)(scratch + o_steps);
+  eb.rng_out = (uint32_t *)(scratch + o_rng);
+  eb.final_items = (int *)(scratch + o_fin);
+  eb.trace = e->trace ? (int *)(scratch + o_trace) : nullptr;
+  eb.trace_cap = e->trace ? e->trace_cap : 0;
+  int st = XH_OK;
+  if (e->init_items) {
+    eb.init_items = (const int *)(scratch + o_init);
+    st = copy_ok(hipMemcpyAsync(scratch + o_init, e->init_items,
+                                4 * (size_t)n * D, hipMemcpyHostToDevice, s));
+  }
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (st == XH_OK) {
+    HIPCHK(hipEventCreate(&ev0));
+    HIPCHK(hipEventCreate(&ev1));
+    HIPCHK(hipEventRecord(ev0, s));
+    const hipError_t le = launch(eb);
+    if (le != hipSuccess)
+      st = fail(XH_ERR_HIP, "evaluate launch: %s", hipGetErrorString(le));
+    HIPCHK(hipEventRecord(ev1, s));
+  }
+  auto out = [&](void *host, size_t off, size_t nb) {
+    if (st == XH_OK && host)
+      st = copy_ok(hipMemcpyAsync(host, scratch + off, nb,
+                                  hipMemcpyDeviceToHost, s));
+  };
+  out(e->totals, 0, sizeof(double) * n);
+  out(e->steps, o_steps, 8 * (size_t)n);
+  out(e->rng_out, o_rng, 4 * (size_t)n);
+  out(e->final_items, o_fin, 4 * (size_t)n * D);
+  out(e->trace, o_trace, 4 * (size_t)eb.trace_cap);
+  (void)hipFreeAsync(scratch, s);
+  HIPCHK(hipStreamSynchronize(s));
+  if (ev0 && ev1) {
+    float ms = 0.0f;
+    if (st == XH_OK && hipEventElapsedTime(&ms, ev0, ev1) == hipSuccess)
+      e->elapsed_ms = ms;
+    hipEventDestroy(ev0);
+    hipEventDestroy(ev1);
+  }
+  return st;
+}
+
 int refresh_value_transpose(xh_trainer *t) {
   return timed(t, "value", [&]() {
     return xh::launch_transpose(t->vp + t->vl.oW1(), t->vw1t, t->vl.V1,
@@ -417,6 +520,13 @@ extern "C" {
 
 const char *xh_last_error(void) { return g_err.c_str(); }
 const char *xh_version(void) { return "xylo-hip 0.1 (gfx950)"; }
+
+size_t xh_struct_size(const char *name) {
+  if (!name) return 0;
+  if (!std::strcmp(name, "xh_config")) return sizeof(xh_config);
+  if (!std::strcmp(name, "xh_eval")) return sizeof(xh_eval);
+  return 0;
+}
 
 int xh_comm_unique_id(void *out128) {
   return guard([&]() -> int {
@@ -573,15 +683,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     // minstd_rand0 seeding rule: s mod m, 0 -> 1
     t->cfg.rng_state = c.rng_state % 2147483647u;
     if (t->cfg.rng_state == 0) t->cfg.rng_state = 1;
-    static const int ia[3][3] = {{4, 0, 0}, {4, 2, 0}, {4, 2, 2}};
-    static const int ib[3][3] = {{1, 0, 0}, {1, 2, 0}, {1, 2, 1}};
-    t->env.B = c.bins;
-    t->env.D = c.dims;
-    for (int d = 0; d < 3; ++d) {
-      t->env.item_a[d] = ia[c.dims - 1][d];
-      t->env.item_b[d] = ib[c.dims - 1][d];
-    }
-    t->env.p_a = 0.4;
+    t->env = make_env(c.bins, c.dims);
     t->pl = xh::PolicyLayout{2 * c.dims, c.policy_h1, c.policy_h2};
     t->vl = xh::ValueLayout{c.bins * 2 * c.dims, c.value_h1, c.value_h2};
     t->np = t->pl.size();
@@ -817,70 +919,59 @@ int xh_trainer_evaluate(xh_trainer *t, xh_eval *e) {
   return guard([&]() -> int {
     if (!t || !e) return fail(XH_ERR_INVALID, "null trainer / eval");
     const int G = t->cfg.bins <= 64 ? 64 / t->cfg.bins : 0;
-    const int n = e->n_envs, D = t->cfg.dims;
     if (G == 0)
       return fail(XH_ERR_INVALID, "evaluate: bins %d > 64 not supported",
                   t->cfg.bins);
-    if (n <= 0 || n % G || e->episodes < 0 || e->trace_cap < 0)
-      return fail(XH_ERR_INVALID, "evaluate: n_envs %d (multiple of %d), "
-                  "episodes %d", n, G, e->episodes);
-    if (e->init_items)
-      for (long i = 0; i < (long)n * D; ++i)
-        if (e->init_items[i] != t->env.item_a[i % D] &&
-            e->init_items[i] != t->env.item_b[i % D])
-          return fail(XH_ERR_INVALID, "evaluate: init_items[%ld] = %d is not "
-                      "an item of the table", i, e->init_items[i]);
-    HIPCHK(hipSetDevice(t->ctx->device));
-    hipStream_t s = t->ctx->stream;
-    // one scratch block: totals | steps | rng | init items | final items | trace
-    const size_t o_steps = sizeof(double) * n, o_rng = o_steps + 8 * (size_t)n,
-                 o_init = o_rng + 4 * (size_t)n,
-                 o_fin = o_init + 4 * (size_t)n * D,
-                 o_trace = o_fin + 4 * (size_t)n * D,
-                 bytes = o_trace + 4 * (size_t)(e->trace ? e->trace_cap : 0);
-    char *scratch = nullptr;
-    HIPCHK(hipMallocAsync((void **)&scratch, bytes, s));
-    xh::EvalArgs a{};
-    a.env = t->env;
-    a.params = t->pp;
-    a.n_envs = n;
-    a.episodes = e->episodes;
-    a.argmax_probs = e->argmax_probs ? 1 : 0;
-    const uint32_t x0 = e->rng_state % 2147483647u;
-    a.x0 = x0 ? x0 : 1u;
-    a.stream_stride = 1ull << 26;
-    // an episode lasts at most B * capacity * D + 1 steps (every step puts
-    // at least one unit into some bin)
-    a.max_steps = (long)(e->episodes + 1) * (t->cfg.bins * 8 * D + 2);
-    a.total = (double *)scratch;
-    a.steps = (long *)(scratch + o_steps);
-    a.rng_out = (uint32_t *)(scratch + o_rng);
-    a.final_items = (int *)(scratch + o_fin);
-    a.trace = e->trace ? (int *)(scratch + o_trace) : nullptr;
-    a.trace_cap = e->trace ? e->trace_cap : 0;
-    int st = XH_OK;
-    if (e->init_items) {
-      a.init_items = (const int *)(scratch + o_init);
-      st = copy_ok(hipMemcpyAsync(scratch + o_init, e->init_items,
-                                  4 * (size_t)n * D, hipMemcpyHostToDevice, s));
-    }
-    if (st == XH_OK)
-      st = timed(t, "evaluate", [&]() {
-        return xh::launch_eval_argmax(a, t->cfg.policy_h1, t->cfg.policy_h2, s);
-      });
-    auto out = [&](void *host, size_t off, size_t nb) {
-      if (st == XH_OK && host)
-        st = copy_ok(hipMemcpyAsync(host, scratch + off, nb,
-                                    hipMemcpyDeviceToHost, s));
-    };
-    out(e->totals, 0, sizeof(double) * n);
-    out(e->steps, o_steps, 8 * (size_t)n);
-    out(e->rng_out, o_rng, 4 * (size_t)n);
-    out(e->final_items, o_fin, 4 * (size_t)n * D);
-    out(e->trace, o_trace, 4 * (size_t)a.trace_cap);
-    (void)hipFreeAsync(scratch, s);
-    HIPCHK(hipStreamSynchronize(s));
-    return st;
+    return eval_common(t->ctx, t->env, G, e, [&](const EvalBuffers &eb) {
+      xh::EvalArgs a{};
+      a.env = t->env;
+      a.params = t->pp;
+      a.n_envs = e->n_envs;
+      a.episodes = e->episodes;
+      a.argmax_probs = e->argmax_probs ? 1 : 0;
+      a.x0 = eb.x0;
+      a.stream_stride = kEvalStride;
+      a.max_steps = eb.max_steps;
+      a.init_items = eb.init_items;
+      a.total = eb.total;
+      a.steps = eb.steps;
+      a.rng_out = eb.rng_out;
+      a.final_items = eb.final_items;
+      a.trace = eb.trace;
+      a.trace_cap = eb.trace_cap;
+      return xh::launch_eval_argmax(a, t->cfg.policy_h1, t->cfg.policy_h2,
+                                    t->ctx->stream);
+    });
+  });
+}
+
+int xh_heuristic_evaluate(xh_ctx *ctx, int policy, int bins, int dims,
+                          xh_eval *e) {
+  return guard([&]() -> int {
+    if (!ctx || !e) return fail(XH_ERR_INVALID, "null ctx / eval");
+    if (policy < XH_HEUR_RANDOM || policy > XH_HEUR_MINWASTE)
+      return fail(XH_ERR_INVALID, "heuristic policy %d", policy);
+    if (!xh::heuristic_shape_supported(bins, dims))
+      return fail(XH_ERR_INVALID, "heuristic: bins %d dims %d not supported",
+                  bins, dims);
+    const xh::EnvDesc env = make_env(bins, dims);
+    return eval_common(ctx, env, 64 / bins, e, [&](const EvalBuffers &eb) {
+      xh::HeuristicArgs a{};
+      a.env = env;
+      a.n_envs = e->n_envs;
+      a.episodes = e->episodes;
+      a.x0 = eb.x0;
+      a.stream_stride = kEvalStride;
+      a.max_steps = eb.max_steps;
+      a.init_items = eb.init_items;
+      a.total = eb.total;
+      a.steps = eb.steps;
+      a.rng_out = eb.rng_out;
+      a.final_items = eb.final_items;
+      a.trace = eb.trace;
+      a.trace_cap = eb.trace_cap;
+      return xh::launch_heuristic(a, policy, ctx->stream);
+    });
   });
 }
 

@@ -70,6 +70,52 @@ class Context:
             pass
 
 
+def _eval_struct(n_envs, episodes, rng_state, D, init_items, trace_cap,
+                 argmax_probs=False):
+    out = {"totals": np.zeros(n_envs, np.float64),
+           "steps": np.zeros(n_envs, np.int64),
+           "final_items": np.zeros((n_envs, D), np.int32),
+           "rng": np.zeros(n_envs, np.uint32),
+           "trace": np.zeros(max(trace_cap, 1), np.int32)}
+    e = _lib.Eval()
+    e.n_envs, e.episodes = n_envs, episodes
+    e.argmax_probs, e.rng_state = 1 if argmax_probs else 0, rng_state
+    keep = []
+    if init_items is not None:
+        init = np.ascontiguousarray(init_items, np.int32).reshape(n_envs, D)
+        keep.append(init)
+        e.init_items = init.ctypes.data
+    e.final_items = out["final_items"].ctypes.data
+    e.rng_out = out["rng"].ctypes.data
+    e.totals = out["totals"].ctypes.data
+    e.steps = out["steps"].ctypes.data
+    if trace_cap > 0:
+        e.trace, e.trace_cap = out["trace"].ctypes.data, trace_cap
+    return e, out, keep
+
+
+def _eval_result(e, out, trace_cap):
+    if trace_cap <= 0:
+        del out["trace"]
+    out["elapsed_ms"] = e.elapsed_ms
+    return out
+
+
+def heuristic_evaluate(ctx, kind, bins, dims, n_envs, episodes, rng_state,
+                       init_items=None, trace_cap=0):
+    """The reference's heuristic agents (firstfit / bestfit / minwaste /
+    random) on the device: n_envs independent envs (multiple of 64/bins),
+    `episodes` episodes each; env 0 reproduces a single-env reference run
+    seeded at rng_state.  Returns totals, steps, final_items, rng, trace,
+    elapsed_ms (device time)."""
+    e, out, keep = _eval_struct(n_envs, episodes, rng_state, dims, init_items,
+                                trace_cap)
+    check(_lib.lib.xh_heuristic_evaluate(ctx.h, _lib.HEURISTICS[kind], bins,
+                                         dims, C.byref(e)))
+    del keep
+    return _eval_result(e, out, trace_cap)
+
+
 def policy_param_count(dims, h1, h2):
     f0 = 2 * dims
     return h1 * f0 + h1 + h2 * h1 + h2 + h2 + 1
@@ -212,30 +258,13 @@ class Trainer:
     def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False,
                  init_items=None, trace_cap=0):
         """Argmax evaluation (deep_agent.cc / the drivers' periodic eval).
-        Returns a dict: totals, steps, final_items, rng (per env) and, with
-        trace_cap > 0, env 0's first trace_cap actions."""
-        D = self.D
-        out = {"totals": np.zeros(n_envs, np.float64),
-               "steps": np.zeros(n_envs, np.int64),
-               "final_items": np.zeros((n_envs, D), np.int32),
-               "rng": np.zeros(n_envs, np.uint32),
-               "trace": np.zeros(max(trace_cap, 1), np.int32)}
-        e = _lib.Eval()
-        e.n_envs, e.episodes = n_envs, episodes
-        e.argmax_probs, e.rng_state = 1 if argmax_probs else 0, rng_state
-        if init_items is not None:
-            init = np.ascontiguousarray(init_items, np.int32).reshape(n_envs, D)
-            e.init_items = init.ctypes.data
-        e.final_items = out["final_items"].ctypes.data
-        e.rng_out = out["rng"].ctypes.data
-        e.totals = out["totals"].ctypes.data
-        e.steps = out["steps"].ctypes.data
-        if trace_cap > 0:
-            e.trace, e.trace_cap = out["trace"].ctypes.data, trace_cap
+        Returns a dict: totals, steps, final_items, rng (per env), env 0's
+        first trace_cap actions (trace_cap > 0), elapsed_ms."""
+        e, out, keep = _eval_struct(n_envs, episodes, rng_state, self.D,
+                                    init_items, trace_cap, argmax_probs)
         check(_lib.lib.xh_trainer_evaluate(self.h, C.byref(e)))
-        if trace_cap <= 0:
-            del out["trace"]
-        return out
+        del keep
+        return _eval_result(e, out, trace_cap)
 
     def seed_streams(self, x):
         """Re-base the env streams on global engine state x (reference order:

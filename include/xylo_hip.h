@@ -167,8 +167,20 @@ typedef struct xh_eval {
   long *steps;               /* [n_envs] or NULL */
   int32_t *trace;            /* [trace_cap] or NULL */
   long trace_cap;
+  double elapsed_ms;         /* out: device time of the evaluation kernel */
 } xh_eval;
 int xh_trainer_evaluate(xh_trainer *t, xh_eval *e);
+
+/* The reference's heuristic agents as device policies, on independent envs
+ * with the stream convention of xh_trainer_evaluate (env 0 reproduces a
+ * single-env reference run): XH_HEUR_RANDOM = xylo::random_policy (rl.h:
+ * 305-316, random_agent.cc), XH_HEUR_FIRSTFIT (firstfit_agent.cc:10-28),
+ * XH_HEUR_BESTFIT (bestfit_agent.cc:10-30), XH_HEUR_MINWASTE
+ * (minwaste_agent.cc:10-39).  bins in {8,16,32,64}, dims 1..3. */
+enum { XH_HEUR_RANDOM = 0, XH_HEUR_FIRSTFIT = 1, XH_HEUR_BESTFIT = 2,
+       XH_HEUR_MINWASTE = 3 };
+int xh_heuristic_evaluate(xh_ctx *ctx, int policy, int bins, int dims,
+                          xh_eval *e);
 
 /* Re-base the per-env engine streams on a global minstd_rand0 state x: the
  * next rollout steps env g (global index) from x advanced by 4*T*g draws, i.e.
@@ -176,6 +188,10 @@ int xh_trainer_evaluate(xh_trainer *t, xh_eval *e);
  * (ppo_training.cc:53-62 run sequentially, 4 draws per step).  After that
  * rollout the global engine is at x advanced by 4*T*num_envs_global. */
 int xh_trainer_seed_streams(xh_trainer *t, uint32_t x);
+
+/* sizeof of the ABI structs ("xh_config", "xh_eval"; 0 if unknown), so a
+ * foreign-language binding can check its mirror of them. */
+size_t xh_struct_size(const char *name);
 
 /* Kernel timing with HIP events on the trainer's stream (off by default). */
 int xh_trainer_set_timing(xh_trainer *t, int on);

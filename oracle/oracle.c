@@ -981,3 +981,66 @@ double or_eval_argmax(const or_env_cfg *c, const or_model *pol,
   }
   return total;
 }
+
+/* The reference's heuristic agents (firstfit_agent.cc:10-28,
+ * bestfit_agent.cc:10-30, minwaste_agent.cc:10-39, random_policy rl.h:
+ * 305-316) playing `episodes` episodes on one env seeded at *x (constructed
+ * first, 2 draws); returns the total reward.  Generalised to D dims as the
+ * device kernel is (bestfit sums item/bin over the dims in order; minwaste's
+ * 0 score = residual with one dim at cap/2 and the others 0). */
+double or_heuristic_eval(const or_env_cfg *c, int kind, long episodes,
+                         uint32_t *x, int32_t *lens) {
+  const int B = c->B, D = c->D;
+  int32_t bins[128 * 3], item[3];
+  float sc[128];
+  double total = 0;
+  or_env_construct(c, bins, item, x);
+  for (long e = 0; e < episodes; ++e) {
+    int32_t len = 0;
+    for (;;) {
+      int ch = 0;
+      if (kind == OR_HEUR_RANDOM) {
+        for (int i = 0; i < B; ++i) sc[i] = (float)(1.0 / B);
+        ch = or_discrete(x, sc, B);
+      } else {
+        for (int i = 0; i < B; ++i) {
+          int fits = 1;
+          for (int d = 0; d < D; ++d) fits &= item[d] <= bins[i * D + d];
+          if (kind == OR_HEUR_FIRSTFIT) {
+            sc[i] = fits ? 1.0f : 0.0f;
+          } else if (kind == OR_HEUR_BESTFIT) {
+            float v = -1.0f;
+            if (fits) {
+              v = (float)item[0] / (float)bins[i * D];
+              for (int d = 1; d < D; ++d)
+                v = v + (float)item[d] / (float)bins[i * D + d];
+            }
+            sc[i] = v;
+          } else {
+            float v = -1.0f;
+            if (fits) {
+              int half = 0, zero = 0;
+              for (int d = 0; d < D; ++d) {
+                const int r = bins[i * D + d] - item[d];
+                half += r == c->cap / 2;
+                zero += r == 0;
+              }
+              v = (half == 1 && zero == D - 1) ? 0.0f : 1.0f;
+            }
+            sc[i] = v;
+          }
+        }
+        ch = or_argmax(sc, B);
+      }
+      or_env_apply(c, bins, item, ch, x);
+      ++len;
+      if (or_env_game_over(c, bins)) {
+        or_env_reset(c, bins, item, x);
+        break;
+      }
+      total += 1.0;
+    }
+    if (lens) lens[e] = len;
+  }
+  return total;
+}

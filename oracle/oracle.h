@@ -141,6 +141,13 @@ void or_value_grad_rows(const or_model *m, const float *params, const float *x,
 double or_eval_argmax(const or_env_cfg *env, const or_model *pol,
                       const float *params, long episodes, uint32_t *x);
 
+/* Heuristic agents (firstfit / bestfit / minwaste / random), one env seeded
+ * at *x: total reward; per-episode lengths into lens (may be NULL). */
+enum { OR_HEUR_RANDOM = 0, OR_HEUR_FIRSTFIT = 1, OR_HEUR_BESTFIT = 2,
+       OR_HEUR_MINWASTE = 3 };
+double or_heuristic_eval(const or_env_cfg *env, int kind, long episodes,
+                         uint32_t *x, int32_t *lens);
+
 #ifdef __cplusplus
 }
 #endif

@@ -284,6 +284,24 @@ def value_grad_rows(model, params, x, targets):
     return g
 
 
+OR_HEUR = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
+
+
+def heuristic_eval(B, D, kind, episodes, x0):
+    """The reference's heuristic agents on one env seeded at x0: (total
+    reward, per-episode lengths, engine state after)."""
+    cfg = env_cfg(B, D)
+    x = C.c_uint32(x0)
+    lens = np.zeros(max(episodes, 1), np.int32)
+    l = lib()
+    l.or_heuristic_eval.restype = C.c_double
+    l.or_heuristic_eval.argtypes = [C.c_void_p, C.c_int, C.c_long,
+                                    C.POINTER(C.c_uint32), C.c_void_p]
+    total = l.or_heuristic_eval(C.byref(cfg), OR_HEUR[kind], episodes,
+                                C.byref(x), _ptr(lens))
+    return total, lens[:episodes], x.value
+
+
 def eval_argmax(B, D, model, params, episodes, x0):
     cfg = env_cfg(B, D)
     x = C.c_uint32(x0)

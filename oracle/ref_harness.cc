@@ -29,6 +29,26 @@
 
 #include <xeno/sys/file_descriptor.h>
 
+// The heuristic policies of the reference's own agent programs
+// (firstfit_agent.cc:10-28, bestfit_agent.cc:10-30, minwaste_agent.cc:10-39),
+// compiled from those files where they lie; their main() is renamed and never
+// called (mode=heuristic drives the policies with a seeded engine instead).
+namespace ref_firstfit {
+#define main firstfit_main
+#include <apps/bin_packing/firstfit_agent.cc>
+#undef main
+}  // namespace ref_firstfit
+namespace ref_bestfit {
+#define main bestfit_main
+#include <apps/bin_packing/bestfit_agent.cc>
+#undef main
+}  // namespace ref_bestfit
+namespace ref_minwaste {
+#define main minwaste_main
+#include <apps/bin_packing/minwaste_agent.cc>
+#undef main
+}  // namespace ref_minwaste
+
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -543,6 +563,47 @@ int mode_random(std::map<std::string, std::string> &a) {
   return 0;
 }
 
+// ---------------------------------------------------- mode: heuristic ------
+// The agent programs' loop (firstfit_agent.cc:30-46 & co.): per round a new
+// env + replay buffer, `episodes` episodes, average reward; seeded.  Records
+// the per-round averages and round 0's episode lengths.
+int mode_heuristic(std::map<std::string, std::string> &a) {
+  recorder rec(a["out"]);
+  xylo::default_generator().seed(iarg(a, "seed", 1));
+  const long rounds = iarg(a, "rounds", 2), episodes = iarg(a, "episodes", 100);
+  const std::string kind = a["policy"];
+  ref_firstfit::firstfit_policy ff;
+  ref_bestfit::bestfit_policy bf;
+  ref_minwaste::minwaste_policy mw;
+  xylo::random_policy<bp::num_bins, bp::observation> rnd;
+  const xylo::policy<bp::action, bp::observation> *pol =
+      kind == "firstfit" ? (const xylo::policy<bp::action, bp::observation> *)&ff
+      : kind == "bestfit" ? (const xylo::policy<bp::action, bp::observation> *)&bf
+      : kind == "minwaste"
+          ? (const xylo::policy<bp::action, bp::observation> *)&mw
+          : (const xylo::policy<bp::action, bp::observation> *)&rnd;
+  std::vector<float> avg;
+  std::vector<int32_t> lens;
+  std::vector<uint32_t> x_round;
+  for (long r = 0; r < rounds; ++r) {
+    x_round.push_back(engine_state());
+    bp::environment env;
+    xylo::replay_buffer<bp::action, bp::observation> rb;
+    bp::agent agent(*pol, env, rb);
+    for (long i = 0; i < episodes; ++i) agent.play_one_episode();
+    auto exp = rb.sample_td();
+    avg.push_back(xylo::total_rewards<bp::action, bp::observation>(exp) /
+                  double(episodes));
+    if (r == 0)
+      for (auto &t : exp) lens.push_back(t.size());
+    rb.forget();
+  }
+  rec.f32("round_avg", avg);
+  rec.i32("episode_len", lens);
+  rec.u32("x_round", x_round);
+  return 0;
+}
+
 // ------------------------------------------------------- mode: learn -------
 struct learn_cfg {
   std::string algo;  // ppo | klppo | ac | pg
@@ -791,6 +852,7 @@ int main(int argc, char **argv) {
   if (mode == "deep") return mode_deep(a);
   if (mode == "driver") return mode_driver(a);
   if (mode == "random") return mode_random(a);
+  if (mode == "heuristic") return mode_heuristic(a);
   if (mode == "learn") return mode_learn(a, false);
   if (mode == "bench") return mode_learn(a, true);
   std::fprintf(stderr, "unknown mode %s\n", mode.c_str());

@@ -92,6 +92,16 @@ FIXTURES = {
     "driver_ppo2_s7": ("driver", ["algo=ppo", "seed=7", "workers=16"]),
     # random_agent.cc's loop seeded: 3 rounds x 100 episodes
     "random_s5": ("random", ["seed=5", "rounds=3", "episodes=100"]),
+    # the reference's own heuristic agents (firstfit/bestfit/minwaste_agent.cc
+    # policies, random_agent.cc's random_policy), seeded: 2 rounds x 1000
+    "heur_firstfit": ("heuristic", ["policy=firstfit", "seed=3", "rounds=2",
+                                    "episodes=1000"]),
+    "heur_bestfit": ("heuristic", ["policy=bestfit", "seed=3", "rounds=2",
+                                   "episodes=1000"]),
+    "heur_minwaste": ("heuristic", ["policy=minwaste", "seed=3", "rounds=2",
+                                    "episodes=1000"]),
+    "heur_random": ("heuristic", ["policy=random", "seed=3", "rounds=2",
+                                  "episodes=1000"]),
     # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])
     "pg_b8d1": ("learn", ["algo=pg", "B=8", "D=1", "widths=32", "N=1",
                           "episodes=4", "iters=3", "seed=17"]),

@@ -171,3 +171,16 @@ def test_free_running_sampling_matches_reference(name):
     """Without teacher forcing the oracle's own sampler reproduces the
     reference's actions (no probability near-ties in these fixtures)."""
     run_oracle_against(name, forced=False)
+
+
+# ----------------------------------------------------------- heuristics ----
+@pytest.mark.parametrize("kind", ["firstfit", "bestfit", "minwaste", "random"])
+def test_heuristic_agents_match_reference(kind):
+    """or_heuristic_eval vs the reference's own agent programs' policies
+    (heur_* fixtures: 2 rounds x 1000 episodes, seed 3)."""
+    g = golden("heur_" + kind)
+    for r in range(2):
+        total, lens, _ = po.heuristic_eval(8, 2, kind, 1000, int(g["x_round"][r]))
+        assert np.float32(total / 1000.0) == g["round_avg"][r]
+        if r == 0:
+            np.testing.assert_array_equal(lens, g["episode_len"])
