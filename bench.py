@@ -81,7 +81,7 @@ def cpu_baseline(seconds_budget=20.0):
                 n_env, T, iters)}
 
 
-def pmc_traffic(kernel="policy_train_kernel"):
+def pmc_traffic(kernel="policy_train"):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     FETCH_SIZE / WRITE_SIZE summary (separate --pmc passes; see
     tools/pmc_summary.py).  Raw counters (FETCH_SIZE is not x2-corrected: the
@@ -92,7 +92,9 @@ def pmc_traffic(kernel="policy_train_kernel"):
     if not files:
         return None, None
     with open(files[-1]) as f:
-        s = json.load(f).get(kernel)
+        summ = json.load(f)
+    # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
+    s = next((v for k, v in sorted(summ.items()) if k.startswith(kernel)), None)
     if not s:
         return None, None
     return s["hbm_bytes"], os.path.relpath(files[-1], REPO)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs into profiles/<tag>_*.{csv,json}.
 
-    python tools/pmc_summary.py <tag> <trace_dir> <fetch_dir> <write_dir>
+    [PROFILE_OUT=dir] python tools/pmc_summary.py <tag> <trace_dir> <fetch_dir> <write_dir>
 
 Per kernel: average duration (kernel trace) and HBM bytes per launch from the
 separate FETCH_SIZE / WRITE_SIZE passes (units: KB; MI355X_MICROARCH.md §HBM:
@@ -14,24 +14,31 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
 
 def per_kernel(path, counter):
     agg = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(path, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
                 agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def short(name):
+    """'void xh::policy_train8_kernel<...>(...)' -> 'policy_train8_kernel'."""
+    m = re.match(r"(?:void )?(?:xh::)?([A-Za-z_0-9]+)", name)
+    return m.group(1) if m else name
+
+
 def main(tag, trace, fetch, write):
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = os.path.join(here, "profiles")
+    out = os.environ.get("PROFILE_OUT", os.path.join(here, "profiles"))
     os.makedirs(out, exist_ok=True)
-    stats = glob.glob(os.path.join(trace, "*kernel_stats.csv"))[0]
+    stats = glob.glob(os.path.join(trace, "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, os.path.join(out, "%s_kernel_stats.csv" % tag))
     dur = {r["Name"]: float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
     fs, ws = per_kernel(fetch, "FETCH_SIZE"), per_kernel(write, "WRITE_SIZE")
@@ -39,12 +46,13 @@ def main(tag, trace, fetch, write):
     for k in sorted(set(fs) | set(ws)):
         fb = fs.get(k, 0.0) * 1024
         wb = ws.get(k, 0.0) * 1024
-        summary[k] = {"avg_ns": dur.get(k), "fetch_bytes_raw": fb,
+        summary[short(k)] = {"kernel": k, "avg_ns": dur.get(k), "fetch_bytes_raw": fb,
                       "fetch_bytes_x2": 2 * fb, "write_bytes": wb,
                       "hbm_bytes": fb + wb, "hbm_bytes_x2_reads": 2 * fb + wb}
     with open(os.path.join(out, "%s_pmc_summary.json" % tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    print(json.dumps(summary.get("policy_train_kernel"), indent=1))
+    print(json.dumps({k: v for k, v in summary.items() if "policy_train" in k},
+                     indent=1))
 
 
 if __name__ == "__main__":
