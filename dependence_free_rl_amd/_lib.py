@@ -15,6 +15,7 @@ XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)
 XH_PPO, XH_AC, XH_KLPPO = 0, 1, 2
 HEURISTICS = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
 XH_POLICY, XH_VALUE = 0, 1
+OPTIMIZERS = {"sgd": 0, "momentum": 1, "adam": 2}
 (BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
  BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
  BUF_LOGITS, BUF_PROBS, BUF_V_STATE0, BUF_QOLD, BUF_KL) = range(17)
@@ -70,6 +71,8 @@ def _load():
         "xh_trainer_num_params": (sz, [vp, i]),
         "xh_trainer_set_params": (i, [vp, i, vp, sz]),
         "xh_trainer_get_params": (i, [vp, i, vp, sz]),
+        "xh_trainer_set_optimizer": (i, [vp, i, i, C.c_float, C.c_float,
+                                         C.c_float, C.c_float]),
         "xh_trainer_rollout": (i, [vp]),
         "xh_trainer_learn": (i, [vp]),
         "xh_trainer_iterate": (i, [vp, i]),

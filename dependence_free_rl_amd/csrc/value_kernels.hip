@@ -286,6 +286,31 @@ __global__ void sgd_kernel(float *p, const float *g, int n, float lr,
     p[i] = p[i] * keep - g[i] * lr;
 }
 
+// momentum_optimizer::next_parameters (nn.h:637-651): v = rho v + g;
+// p - v * lr.  adam_optimizer::next_parameters (nn.h:666-691): m, v moments,
+// bias-corrected by c1 = 1 - beta1^t, c2 = 1 - beta2^t; p - m^ lr /
+// (sqrt(v^) + 1e-7).  One element per lane, the reference's operation order.
+__global__ void opt_kernel(float *p, const float *g, float *m, float *v, int n,
+                           OptStep o) {
+#pragma clang fp contract(off)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    if (o.kind == 1) {
+      const float vel = 0.9f * m[i] + gi;
+      m[i] = vel;
+      p[i] = p[i] - vel * o.lr;
+    } else {
+      const float m1 = m[i] * o.beta1 + gi * (1.0f - o.beta1);
+      const float m2 = v[i] * o.beta2 + gi * gi * (1.0f - o.beta2);
+      m[i] = m1;
+      v[i] = m2;
+      const float mu = m1 / o.c1, vu = m2 / o.c2;
+      p[i] = p[i] - mu * o.lr / (sqrtf(vu) + 1e-7f);
+    }
+  }
+}
+
 // ----------------------------------------------------------- launchers ----
 bool value_shape_supported(int V1, int V2) {
   return (V1 == 64 && V2 == 32) || (V1 == 32 && V2 == 32);
@@ -378,6 +403,13 @@ hipError_t launch_sgd(float *params, const float *grad, int n, float lr,
                       float wd, hipStream_t s) {
   hipLaunchKernelGGL(sgd_kernel, dim3(blocks_for(n)), dim3(256), 0, s, params,
                      grad, n, lr, wd);
+  return hipGetLastError();
+}
+
+hipError_t launch_opt(float *params, const float *grad, float *m, float *v,
+                      int n, OptStep o, hipStream_t s) {
+  hipLaunchKernelGGL(opt_kernel, dim3(blocks_for(n)), dim3(256), 0, s, params,
+                     grad, m, v, n, o);
   return hipGetLastError();
 }
 

@@ -200,5 +200,14 @@ hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s);
 hipError_t launch_sgd(float *params, const float *grad, int n, float lr,
                       float wd, hipStream_t s);
+// momentum_optimizer (kind 1) / adam_optimizer (kind 2), nn.h:630-698: state
+// m (velocity / first moment) and v (second moment); c1, c2 = adam's bias
+// corrections 1 - beta^t computed on the host as the reference does.
+struct OptStep {
+  int kind;
+  float lr, beta1, beta2, c1, c2;
+};
+hipError_t launch_opt(float *params, const float *grad, float *m, float *v,
+                      int n, OptStep o, hipStream_t s);
 
 }  // namespace xh

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -132,6 +133,13 @@ struct xh_trainer {
   float *qold = nullptr, *beta = nullptr, *kl_log = nullptr;
   int *end_list = nullptr, *n_end = nullptr, *n_open = nullptr;
   double *kl_part = nullptr, *kl_sum = nullptr;
+  // optimizers of the policy [0] and value [1] nets (nn.h:589-698)
+  struct opt_state {
+    int kind = XH_OPT_SGD;
+    float lr = 0, wd = 0, beta1 = 0.9f, beta2 = 0.999f;
+    float t = 1.0f;                    // adam_optimizer::t (nn.h:694)
+    float *m = nullptr, *v = nullptr;  // velocity / moments (device)
+  } opt[2];
   uint32_t jump_mul = 1;
   int rgrid = 0;
   bool need_shift = false;
@@ -382,6 +390,26 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
   return st;
 }
 
+// optimizer::step's next_parameters for net `which` (nn.h:594-698).
+int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
+              int n) {
+  hipStream_t s = t->ctx->stream;
+  auto &o = t->opt[which];
+  if (o.kind == XH_OPT_SGD)
+    return timed(t, "reduce_sgd", [&]() {
+      return xh::launch_sgd(params, grad, n, o.lr, o.wd, s);
+    });
+  xh::OptStep st{o.kind, o.lr, o.beta1, o.beta2, 1.0f, 1.0f};
+  if (o.kind == XH_OPT_ADAM) {  // host float powf, as the reference
+    st.c1 = 1 - powf(o.beta1, o.t);
+    st.c2 = 1 - powf(o.beta2, o.t);
+    o.t += 1;
+  }
+  return timed(t, "reduce_sgd", [&]() {
+    return xh::launch_opt(params, grad, o.m, o.v, n, st, s);
+  });
+}
+
 int refresh_value_transpose(xh_trainer *t) {
   return timed(t, "value", [&]() {
     return xh::launch_transpose(t->vp + t->vl.oW1(), t->vw1t, t->vl.V1,
@@ -444,9 +472,7 @@ int do_learn(xh_trainer *t) {
                                   t->vgrad, s);
   }));
   CHK(allreduce(t, t->vgrad, t->nv));
-  CHK(timed(t, "reduce_sgd", [&]() {
-    return xh::launch_sgd(t->vp, t->vgrad, t->nv, c.lr_value, c.wd_value, s);
-  }));
+  CHK(opt_apply(t, XH_VALUE, t->vp, t->vgrad, t->nv));
   CHK(refresh_value_transpose(t));
   // calculate_advantage (policy_gradient.h:220-281): post-update values
   va.v_state = t->v_state;
@@ -505,9 +531,7 @@ int do_learn(xh_trainer *t) {
                                          t->kl_log + 3 * e, s);
       }));
     }
-    CHK(timed(t, "reduce_sgd", [&]() {
-      return xh::launch_sgd(t->pp, g, t->np, c.lr_policy, c.wd_policy, s);
-    }));
+    CHK(opt_apply(t, XH_POLICY, t->pp, g, t->np));
   }
   t->need_shift = true;
   return XH_OK;
@@ -746,6 +770,10 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     }
     if (st == XH_OK && t->beta)
       st = copy_ok(hipMemcpy(t->beta, &c.kl_beta, 4, hipMemcpyHostToDevice));
+    t->opt[XH_POLICY].lr = c.lr_policy;
+    t->opt[XH_POLICY].wd = c.wd_policy;
+    t->opt[XH_VALUE].lr = c.lr_value;
+    t->opt[XH_VALUE].wd = c.wd_value;
     if (st != XH_OK) {
       std::string keep = g_err;
       xh_trainer_destroy(t);
@@ -820,6 +848,41 @@ int xh_trainer_get_params(xh_trainer *t, int which, float *host, size_t n) {
     HIPCHK(hipSetDevice(t->ctx->device));
     HIPCHK(hipMemcpyAsync(host, which == XH_POLICY ? t->pp : t->vp, n * 4,
                           hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHK(hipStreamSynchronize(t->ctx->stream));
+    return XH_OK;
+  });
+}
+
+int xh_trainer_set_optimizer(xh_trainer *t, int which, int kind, float lr,
+                             float weight_decay, float beta1, float beta2) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    if (which != XH_POLICY && which != XH_VALUE)
+      return fail(XH_ERR_INVALID, "optimizer: which %d", which);
+    if (kind != XH_OPT_SGD && kind != XH_OPT_MOMENTUM && kind != XH_OPT_ADAM)
+      return fail(XH_ERR_INVALID, "optimizer: kind %d", kind);
+    if (kind != XH_OPT_SGD && weight_decay != 0.0f)
+      return fail(XH_ERR_INVALID, "optimizer: weight decay is an "
+                  "sgd_optimizer parameter only (nn.h:616-628)");
+    HIPCHK(hipSetDevice(t->ctx->device));
+    auto &o = t->opt[which];
+    const int n = which == XH_POLICY ? t->np : t->nv;
+    if (kind != XH_OPT_SGD && !o.m) {
+      CHK(dalloc(t, &o.m, (size_t)n * 4));
+      CHK(dalloc(t, &o.v, (size_t)n * 4));
+    }
+    if (o.m) {  // fresh state: the reference emplaces zeros on the first step
+      HIPCHK(hipMemsetAsync(o.m, 0, (size_t)n * 4, t->ctx->stream));
+      HIPCHK(hipMemsetAsync(o.v, 0, (size_t)n * 4, t->ctx->stream));
+    }
+    o.kind = kind;
+    o.lr = lr;
+    o.wd = weight_decay;
+    o.beta1 = beta1;
+    o.beta2 = beta2;
+    o.t = 1.0f;
+    (which == XH_POLICY ? t->cfg.lr_policy : t->cfg.lr_value) = lr;
+    (which == XH_POLICY ? t->cfg.wd_policy : t->cfg.wd_value) = weight_decay;
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     return XH_OK;
   });

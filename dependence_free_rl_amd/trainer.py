@@ -201,6 +201,13 @@ class Trainer:
         check(_lib.lib.xh_trainer_get_params(self.h, which, _ptr(out), out.size))
         return out
 
+    def set_optimizer(self, which, kind, lr, weight_decay=0.0, beta1=0.9,
+                      beta2=0.999):
+        """kind: "sgd" | "momentum" | "adam" (nn.h:616-698); fresh state."""
+        check(_lib.lib.xh_trainer_set_optimizer(
+            self.h, which, _lib.OPTIMIZERS[kind], lr, weight_decay, beta1,
+            beta2))
+
     # -------------------------------------------------------------- loop --
     def rollout(self):
         check(_lib.lib.xh_trainer_rollout(self.h))

@@ -334,10 +334,6 @@ class session {
                              "softmax_cross_entropy_layer head"
                            : "xylo-hip: ppo_learner / kl_ppo_learner need a "
                              "softmax_layer head");
-    for (xylo::optimizer *o :
-         {learner_.action_optimizer, learner_.value_optimizer})
-      if (o->kind() != xylo::optimizer_kind::sgd)
-        throw xeno::error("xylo-hip: only sgd_optimizer runs on the device");
     xh_config c;
     xh_config_default(&c, ac ? XH_AC : klppo ? XH_KLPPO : XH_PPO,
                       int(num_bins), 2, N, T_);
@@ -352,6 +348,18 @@ class session {
     c.gamma = learner_.gamma;
     c.lambda = learner_.lambda;
     tr_ = std::make_unique<trainer>(c);
+    // momentum / adam optimizers (nn.h:630-698) run on the device too; their
+    // state starts at zero with the first learn(), as the reference's does
+    for (int which : {XH_POLICY, XH_VALUE}) {
+      xylo::optimizer *o = which == XH_POLICY ? learner_.action_optimizer
+                                              : learner_.value_optimizer;
+      if (o->kind() == xylo::optimizer_kind::sgd) continue;
+      const int kind = o->kind() == xylo::optimizer_kind::adam ? XH_OPT_ADAM
+                                                               : XH_OPT_MOMENTUM;
+      check(xh_trainer_set_optimizer(tr_->h, which, kind, o->rate(), 0.0f,
+                                     o->beta1(), o->beta2()),
+            "xh_trainer_set_optimizer");
+    }
     // initial env states: slot 0 from the host envs (drawn by their ctors)
     const int B = int(num_bins);
     std::vector<std::int8_t> bins(std::size_t(T_ + 1) * N * B * 2, 0),

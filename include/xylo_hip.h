@@ -100,6 +100,18 @@ int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
                           size_t n);
 int xh_trainer_get_params(xh_trainer *t, int which, float *host, size_t n);
 
+/* Optimizer of the policy (XH_POLICY) or value (XH_VALUE) net, replacing
+ * xylo::sgd_optimizer / momentum_optimizer / adam_optimizer (nn.h:616-698)
+ * passed to the learner constructor.  Default: sgd with the xh_config lr /
+ * wd.  momentum: v = 0.9 v + g, p - lr v.  adam: moments with beta1, beta2,
+ * bias-corrected with the step counter t = 1, 2, ... of this optimizer,
+ * p - lr m^ / (sqrt(v^) + 1e-7).  weight_decay must be 0 unless sgd.  The
+ * state (velocity, moments, t) restarts from zero at this call and then
+ * persists across learn() calls, as the reference optimizer object's does. */
+enum { XH_OPT_SGD = 0, XH_OPT_MOMENTUM = 1, XH_OPT_ADAM = 2 };
+int xh_trainer_set_optimizer(xh_trainer *t, int which, int kind, float lr,
+                             float weight_decay, float beta1, float beta2);
+
 /* One iteration's rollout: T steps of every env (one kernel per step). */
 int xh_trainer_rollout(xh_trainer *t);
 /* learn(): value step, advantages, `epochs` policy steps; then the batch's

@@ -370,6 +370,48 @@ void or_sgd(float *params, const float *grad, size_t n, float lr, float wd) {
   for (size_t i = 0; i < n; ++i) params[i] = params[i] * keep - grad[i] * lr;
 }
 
+/* momentum_optimizer / adam_optimizer::next_parameters (nn.h:630-698).
+ * State is created zeroed on the first step (velocity_ / first_moment_ /
+ * second_moment_ emplace); adam's step counter t starts at 1 (nn.h:694) and
+ * is a float, as in the reference. */
+void or_opt_step(or_opt *o, float *params, const float *grad, size_t n) {
+  if (o->kind == OR_OPT_SGD) {
+    or_sgd(params, grad, n, o->lr, o->wd);
+    return;
+  }
+  if (!o->m) {
+    o->m = (float *)calloc(n, sizeof(float));
+    o->v = (float *)calloc(n, sizeof(float));
+    o->t = 1.0f;
+  }
+  if (o->kind == OR_OPT_MOMENTUM) { /* v = 0.9 v + g; p - v*lr (nn.h:644-650) */
+    const float rho = 0.9f;
+    for (size_t i = 0; i < n; ++i) {
+      o->m[i] = rho * o->m[i];
+      o->m[i] = o->m[i] + grad[i];
+      params[i] = params[i] - o->m[i] * o->lr;
+    }
+    return;
+  }
+  /* adam (nn.h:677-690) */
+  const float b1 = o->b1, b2 = o->b2;
+  const float c1 = 1 - powf(b1, o->t), c2 = 1 - powf(b2, o->t);
+  for (size_t i = 0; i < n; ++i) {
+    const float g = grad[i];
+    o->m[i] = o->m[i] * b1 + g * (1 - b1);
+    o->v[i] = o->v[i] * b2 + g * g * (1 - b2);
+    const float m1 = o->m[i] / c1, m2 = o->v[i] / c2;
+    params[i] = params[i] - m1 * o->lr / (sqrtf(m2) + 1e-7f);
+  }
+  o->t += 1;
+}
+
+void or_opt_free(or_opt *o) {
+  free(o->m);
+  free(o->v);
+  o->m = o->v = NULL;
+}
+
 /* --------------------------------------------------------------- trainer -- */
 typedef struct {
   int32_t *bins; /* B*D */
@@ -403,8 +445,9 @@ struct or_trainer {
   or_model pol, val;
   float *pp, *vp; /* params */
   size_t np, nv;
-  float lr_pi, lr_v, wd_pi, wd_v, gamma, lambda;
+  float gamma, lambda;
   float beta, d_targ; /* kl_ppo_learner (policy_gradient.h:332-333) */
+  or_opt opt[2];      /* policy, value optimizers */
   uint32_t x;
   /* workers */
   int32_t *bins, *item; /* N*B*D, N*D */
@@ -472,12 +515,13 @@ or_trainer *or_trainer_create(int algo, const or_env_cfg *env, int N, int T,
     t->vp = (float *)malloc(sizeof(float) * t->nv);
     memcpy(t->vp, val_params, sizeof(float) * t->nv);
   }
-  t->lr_pi = lr_pi;
-  t->lr_v = lr_v;
-  t->wd_pi = wd_pi;
-  t->wd_v = wd_v;
   t->gamma = gamma;
   t->lambda = 0.95f; /* policy_gradient.h:286 */
+  t->opt[0].kind = t->opt[1].kind = OR_OPT_SGD;
+  t->opt[0].lr = lr_pi;
+  t->opt[0].wd = wd_pi;
+  t->opt[1].lr = lr_v;
+  t->opt[1].wd = wd_v;
   t->beta = 1.0f;
   t->d_targ = 1e-9f;
   t->x = x0;
@@ -517,7 +561,21 @@ void or_trainer_destroy(or_trainer *t) {
   free(t->item);
   free(t->steps);
   free(t->cur);
+  or_opt_free(&t->opt[0]);
+  or_opt_free(&t->opt[1]);
   free(t);
+}
+
+void or_trainer_set_optimizer(or_trainer *t, int which, int kind, float lr,
+                              float wd, float beta1, float beta2) {
+  or_opt *o = &t->opt[which ? 1 : 0];
+  or_opt_free(o);
+  o->kind = kind;
+  o->lr = lr;
+  o->wd = wd;
+  o->b1 = beta1;
+  o->b2 = beta2;
+  o->t = 1.0f;
 }
 
 uint32_t or_trainer_rng(const or_trainer *t) { return t->x; }
@@ -816,7 +874,7 @@ void or_trainer_learn(or_trainer *t) {
     pl_ctx pc = {choice, pold, adv, 0, NULL, NULL, 0, 0};
     or_model_grad(&t->pol, t->pp, sm, rows, len, loss_policy, &pc, pgrad);
     buf_append(&t->buf[OR_BUF_POLICY_GRADS], pgrad, t->np, sizeof(float));
-    or_sgd(t->pp, pgrad, t->np, t->lr_pi, t->wd_pi);
+    or_opt_step(&t->opt[0], t->pp, pgrad, t->np);
   } else {
     /* update_value_model (policy_gradient.h:196-218) */
     float *values = (float *)malloc(sizeof(float) * rows);
@@ -838,7 +896,7 @@ void or_trainer_learn(or_trainer *t) {
     sq_ctx sc = {targets};
     or_model_grad(&t->val, t->vp, sm, rows, len, loss_square, &sc, vgrad);
     buf_set(&t->buf[OR_BUF_VALUE_GRAD], vgrad, t->nv, sizeof(float));
-    or_sgd(t->vp, vgrad, t->nv, t->lr_v, t->wd_v);
+    or_opt_step(&t->opt[1], t->vp, vgrad, t->nv);
     free(vgrad);
 
     /* calculate_advantage (policy_gradient.h:220-281), post-update values */
@@ -900,7 +958,7 @@ void or_trainer_learn(or_trainer *t) {
         const float kl[3] = {beta_used, (float)pc.d_avg, t->beta};
         buf_append(&t->buf[OR_BUF_KL], kl, 3, sizeof(float));
       }
-      or_sgd(t->pp, pgrad, t->np, t->lr_pi, t->wd_pi);
+      or_opt_step(&t->opt[0], t->pp, pgrad, t->np);
     }
   }
   buf_set(&t->buf[OR_BUF_ADVANTAGES], adv, rows, sizeof(float));

@@ -78,6 +78,15 @@ void or_model_grad(const or_model *m, const float *params, const float *x,
                    int rows, int xcols, or_loss_fn loss, void *ctx,
                    float *grad);
 void or_sgd(float *params, const float *grad, size_t n, float lr, float wd);
+/* sgd / momentum / adam optimizers (nn.h:616-698) with their state. */
+enum { OR_OPT_SGD = 0, OR_OPT_MOMENTUM = 1, OR_OPT_ADAM = 2 };
+typedef struct {
+  int kind;
+  float lr, wd, b1, b2, t;
+  float *m, *v; /* velocity / first, second moment (NULL until first step) */
+} or_opt;
+void or_opt_step(or_opt *o, float *params, const float *grad, size_t n);
+void or_opt_free(or_opt *o);
 
 /* --------------------------------------------------------------- learner -- */
 enum { OR_PPO = 0, OR_AC = 1, OR_PG = 2, OR_KLPPO = 3 };
@@ -91,6 +100,9 @@ or_trainer *or_trainer_create(int algo, const or_env_cfg *env, int N, int T,
                               float wd_pi, float wd_v, float gamma,
                               uint32_t x0);
 void or_trainer_destroy(or_trainer *t);
+/* Replace the policy (which = 0) or value (1) optimizer; its state restarts. */
+void or_trainer_set_optimizer(or_trainer *t, int which, int kind, float lr,
+                              float wd, float beta1, float beta2);
 /* Rollout of one iteration: workers stepped one after another. If `forced`
  * is non-NULL it supplies the actions (env-major, T per env; the sampler's 2
  * engine draws are still consumed). */

@@ -14,6 +14,7 @@ LIB = os.path.join(HERE, "liboracle.so")
 
 OR_FULL, OR_POINT, OR_RELU, OR_SOFTMAX, OR_SOFTMAX_XENT = range(5)
 OR_PPO, OR_AC, OR_PG, OR_KLPPO = range(4)
+OPT_SGD, OPT_MOMENTUM, OPT_ADAM = range(3)
 (BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE, BUF_STEP_PCHOICE,
  BUF_ROWS, BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_VALUES, BUF_TARGETS,
  BUF_VALUE_GRAD, BUF_ADVANTAGES, BUF_POLICY_GRADS, BUF_FINAL_BINS,
@@ -228,6 +229,14 @@ class Trainer:
             lib().or_trainer_destroy(self.h)
             self.h = None
 
+    def set_optimizer(self, which, kind, lr, wd=0.0, beta1=0.9, beta2=0.999):
+        """kind: OPT_SGD / OPT_MOMENTUM / OPT_ADAM (nn.h:616-698)."""
+        l = lib()
+        l.or_trainer_set_optimizer.argtypes = [C.c_void_p, C.c_int, C.c_int,
+                                               C.c_float, C.c_float, C.c_float,
+                                               C.c_float]
+        l.or_trainer_set_optimizer(self.h, which, kind, lr, wd, beta1, beta2)
+
     def rollout(self, forced=None):
         if forced is not None:
             forced = np.ascontiguousarray(forced, np.int32)
@@ -259,6 +268,29 @@ class Trainer:
             return np.zeros(0, dt)
         arr = (C.c_int32 if dt == np.int32 else C.c_float) * n.value
         return np.frombuffer(arr.from_address(p), dt).copy()
+
+
+class Opt(C.Structure):
+    """or_opt: an optimizer with its state (nn.h:616-698)."""
+    _fields_ = [("kind", C.c_int), ("lr", C.c_float), ("wd", C.c_float),
+                ("b1", C.c_float), ("b2", C.c_float), ("t", C.c_float),
+                ("m", C.c_void_p), ("v", C.c_void_p)]
+
+    def __init__(self, kind, lr, wd=0.0, beta1=0.9, beta2=0.999):
+        super().__init__(kind, lr, wd, beta1, beta2, 1.0, None, None)
+
+    def step(self, params, grad):
+        """In place on the float32 array `params`."""
+        grad = np.ascontiguousarray(grad, np.float32)
+        l = lib()
+        l.or_opt_step.argtypes = [C.POINTER(Opt), C.c_void_p, C.c_void_p,
+                                  C.c_size_t]
+        l.or_opt_step(C.byref(self), _ptr(params), _ptr(grad), params.size)
+
+    def __del__(self):
+        l = lib()
+        l.or_opt_free.argtypes = [C.POINTER(Opt)]
+        l.or_opt_free(C.byref(self))
 
 
 def policy_grad_rows(model, params, x, choice, pold, adv, algo):

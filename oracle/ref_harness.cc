@@ -268,18 +268,49 @@ private:
   }
 };
 
-// Records every flat gradient handed to the optimizer (nn.h:594-605).
-struct recording_sgd : xylo::sgd_optimizer {
-  recording_sgd(xylo::model &m, float rate, float wd = 0.0f)
-      : xylo::sgd_optimizer(m, rate, wd) {}
+// Records every flat gradient handed to the optimizer (nn.h:594-605); the
+// update itself is the reference optimizer's own next_parameters.
+struct grad_log {
   std::vector<std::vector<float>> grads;
   bool record = true;
+};
+
+template <class Base>
+struct recording : Base, grad_log {
+  template <class... Args>
+  recording(xylo::model &m, Args... args) : Base(m, args...) {}
 
 protected:
   xylo::vector next_parameters(const xylo::vector &p, const xylo::vector &g,
                                float rate) override {
     if (record) grads.push_back(std::vector<float>(g.begin(), g.end()));
-    return xylo::sgd_optimizer::next_parameters(p, g, rate);
+    return Base::next_parameters(p, g, rate);
+  }
+};
+using recording_sgd = recording<xylo::sgd_optimizer>;
+
+// opt = sgd | momentum | adam (nn.h:616-698).  Owns the concrete object
+// (xylo::optimizer has no virtual destructor).
+struct opt_holder {
+  std::unique_ptr<recording_sgd> sgd;
+  std::unique_ptr<recording<xylo::momentum_optimizer>> mom;
+  std::unique_ptr<recording<xylo::adam_optimizer>> adam;
+  xylo::optimizer *opt = nullptr;
+  grad_log *log = nullptr;
+  opt_holder(const std::string &kind, xylo::model &m, float lr, float wd) {
+    if (kind == "momentum") {
+      mom = std::make_unique<recording<xylo::momentum_optimizer>>(m, lr);
+      opt = mom.get();
+      log = mom.get();
+    } else if (kind == "adam") {
+      adam = std::make_unique<recording<xylo::adam_optimizer>>(m, lr);
+      opt = adam.get();
+      log = adam.get();
+    } else {
+      sgd = std::make_unique<recording_sgd>(m, lr, wd);
+      opt = sgd.get();
+      log = sgd.get();
+    }
   }
 };
 
@@ -613,6 +644,7 @@ struct learn_cfg {
   uint32_t seed;
   bool record;
   int episodes;  // pg: episodes per worker per iteration
+  std::string opt_pi = "sgd", opt_v = "sgd";  // sgd | momentum | adam
 };
 
 template <std::size_t B, std::size_t D>
@@ -631,8 +663,11 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     build_perbin(pol, f0, c.widths,
                  c.algo == "ac" ? head_softmax_xent : head_softmax);
   if (!pg) build_full(val, B * f0, c.vwidths, 1, head_none);
-  recording_sgd opt_pi(pol, c.lr_pi, c.wd_pi), opt_v(val, c.lr_v, c.wd_v);
-  opt_pi.record = opt_v.record = rec != nullptr;
+  opt_holder hold_pi(c.opt_pi, pol, c.lr_pi, c.wd_pi),
+      hold_v(c.opt_v, val, c.lr_v, c.wd_v);
+  grad_log *log_pi = hold_pi.log, *log_v = hold_v.log;
+  xylo::optimizer &opt_pi = *hold_pi.opt, &opt_v = *hold_v.opt;
+  log_pi->record = log_v->record = rec != nullptr;
 
   if (rec) {
     rec->f32("init_policy", to_std(pol.parameters()));
@@ -763,8 +798,8 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
       rec->f32(p + "step_distrib", lp, {ns, B});
     }
 
-    opt_pi.grads.clear();
-    opt_v.grads.clear();
+    log_pi->grads.clear();
+    log_v->grads.clear();
     if (pg) {
       xylo::vector adv = pgl->get_advantages(exp);
       rec->f32(p + "advantages", to_std(adv));
@@ -772,16 +807,17 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     } else {
       rec->f32(p + "values_before", to_std(val.eval(sm)));
       ac->update_value_model(exp, sm);
-      rec->f32(p + "value_grad", opt_v.grads.at(0));
+      rec->f32(p + "value_grad", log_v->grads.at(0));
       rec->f32(p + "value_params", to_std(val.parameters()));
       xylo::vector adv = ac->calculate_advantage(exp, sm);
       rec->f32(p + "advantages", to_std(adv));
       ac->optimize_action(sm, actions, adv);
     }
     std::vector<float> gall;
-    for (auto &gv : opt_pi.grads) gall.insert(gall.end(), gv.begin(), gv.end());
+    for (auto &gv : log_pi->grads) gall.insert(gall.end(), gv.begin(), gv.end());
     rec->f32(p + "policy_grads", gall,
-             {opt_pi.grads.size(), opt_pi.grads.empty() ? 0 : opt_pi.grads[0].size()});
+             {log_pi->grads.size(),
+              log_pi->grads.empty() ? 0 : log_pi->grads[0].size()});
     rec->f32(p + "policy_params", to_std(pol.parameters()));
     rb.forget();
     rec->u32(p + "x_end", {engine_state()});
@@ -819,6 +855,8 @@ int mode_learn(std::map<std::string, std::string> &a, bool bench) {
   c.gamma = darg(a, "gamma", 0.99);
   c.seed = iarg(a, "seed", 42);
   c.episodes = iarg(a, "episodes", 1);
+  if (a.count("opt_pi")) c.opt_pi = a["opt_pi"];
+  if (a.count("opt_v")) c.opt_v = a["opt_v"];
   int B = iarg(a, "B", 8), D = iarg(a, "D", 2);
   std::unique_ptr<recorder> rec;
   if (!bench) rec = std::make_unique<recorder>(a["out"]);

@@ -102,6 +102,15 @@ FIXTURES = {
                                     "episodes=1000"]),
     "heur_random": ("heuristic", ["policy=random", "seed=3", "rounds=2",
                                   "episodes=1000"]),
+    # the reference's other optimizers (nn.h:630-698) in the learners: PPO
+    # with adam on the policy and momentum on the value net, AC the other
+    # way round; state (moments, velocity, adam's t) carries across learn()
+    "ppo_adam_b8d2": ("learn", ["algo=ppo", "B=8", "D=2", "widths=128,64",
+                                "N=8", "T=8", "iters=3", "seed=23",
+                                "opt_pi=adam", "opt_v=momentum"]),
+    "ac_mom_b8d2": ("learn", ["algo=ac", "B=8", "D=2", "widths=64,32",
+                              "N=16", "T=8", "iters=3", "seed=29",
+                              "opt_pi=momentum", "opt_v=adam"]),
     # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])
     "pg_b8d1": ("learn", ["algo=pg", "B=8", "D=1", "widths=32", "N=1",
                           "episodes=4", "iters=3", "seed=17"]),

@@ -21,7 +21,17 @@ def trainer_from_golden(ctx, name, **kw):
                  widths=widths, rng_state=int(g["x0"][0]), **kw)
     tr.set_params(POLICY, g["init_policy"])
     tr.set_params(VALUE, g["init_value"])
+    for which, key in ((POLICY, "opt_pi"), (VALUE, "opt_v")):
+        if key in kv:
+            tr.set_optimizer(which, kv[key], default_lr(kv["algo"], which))
     return tr, g, kv
+
+
+def default_lr(algo, which):
+    """Drivers' learning rates: ppo_training.cc:17,26 / ac_training.cc:17,26."""
+    if algo == "ac":
+        return 1e-5 if which == 0 else 1e-4
+    return 1e-4 if which == 0 else 1e-5
 
 
 def step_major(arr, N, T):

@@ -10,7 +10,7 @@ values, advantages, gradients, parameters.
 import numpy as np
 import pytest
 
-from conftest import assert_close, golden
+from conftest import assert_close, assert_params_close, golden, noise_mask
 from gpu_helpers import meta, row_index, step_major, trainer_from_golden
 
 pytestmark = pytest.mark.gpu
@@ -98,16 +98,23 @@ def test_rollout_sampling_matches_reference(ctx, name):
 
 
 @pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2",
-                                  "ac_b128d3", "klppo_b8d2"])
+                                  "ac_b128d3", "klppo_b8d2", "ppo_adam_b8d2",
+                                  "ac_mom_b8d2"])
 def test_learn_matches_reference(ctx, name):
     """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
-    value gradient and updated parameters vs the reference learner."""
+    value gradient and updated parameters vs the reference learner (sgd, and
+    momentum / adam optimizers with their state carried across learn();
+    adam's noise-level entries per conftest.noise_mask)."""
     from dependence_free_rl_amd.trainer import (BUF_ADV, BUF_POLICY_GRADS,
                                                 BUF_V_STATE0, BUF_V_TERM,
                                                 BUF_VALUE_GRAD, POLICY, VALUE)
+    from gpu_helpers import default_lr
     tr, g, kv = trainer_from_golden(ctx, name)
     N, T = tr.N, tr.T
     worst = {}
+    adam = {w: kv.get(k) == "adam" for w, k in ((POLICY, "opt_pi"),
+                                               (VALUE, "opt_v"))}
+    mask, nsteps = {POLICY: None, VALUE: None}, {POLICY: 0, VALUE: 0}
     for it in range(int(kv["iters"])):
         p = "it%d_" % it
         tr.set_forced_actions(step_major(g[p + "step_choice"], N, T))
@@ -127,13 +134,20 @@ def test_learn_matches_reference(ctx, name):
             ("values", np.array(vrow), g[p + "values_before"]),
             ("advantages", np.array(arow), g[p + "advantages"]),
             ("value_grad", tr.buffer(BUF_VALUE_GRAD), g[p + "value_grad"]),
-            ("value_params", tr.params(VALUE), g[p + "value_params"]),
             ("policy_grads", tr.buffer(BUF_POLICY_GRADS), g[p + "policy_grads"]),
-            ("policy_params", tr.params(POLICY), g[p + "policy_params"]),
         ]
         for what, x, y in checks:
             worst[what] = max(worst.get(what, 0.0),
                               assert_close(x, y, what=p + what))
+        for w, what, gk in ((VALUE, "value_params", "value_grad"),
+                            (POLICY, "policy_params", "policy_grads")):
+            gr = g[p + gk]
+            nsteps[w] += gr.reshape(-1, gr.shape[-1]).shape[0]
+            if adam[w]:
+                mask[w] = noise_mask(gr, mask[w])
+            worst[what] = max(worst.get(what, 0.0), assert_params_close(
+                tr.params(w), g[p + what], mask[w],
+                2 * default_lr(kv["algo"], w) * nsteps[w], what=p + what))
     print(name, {k: "%.2e" % v for k, v in worst.items()})
 
 

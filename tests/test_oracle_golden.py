@@ -7,7 +7,7 @@ tests/golden/make_golden.py.  CPU only.
 import numpy as np
 import pytest
 
-from conftest import assert_close, golden
+from conftest import assert_close, assert_params_close, golden, noise_mask
 from oracle import pyoracle as po
 
 
@@ -104,8 +104,9 @@ def test_weights20_logits_and_argmax_episodes():
 
 # ------------------------------------------------------------- learners ----
 LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1",
-         "klppo_b8d2"]
+         "klppo_b8d2", "ppo_adam_b8d2", "ac_mom_b8d2"]
 ALGO = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG, "klppo": po.OR_KLPPO}
+OPT = {"sgd": po.OPT_SGD, "momentum": po.OPT_MOMENTUM, "adam": po.OPT_ADAM}
 
 
 def run_oracle_against(name, forced=True):
@@ -122,8 +123,15 @@ def run_oracle_against(name, forced=True):
                     lr_v=lr_v, wd_pi=float(kv.get("wd_pi", 0.0)), gamma=0.99,
                     x0=int(g["x0"][0]),
                     episodes=int(kv.get("episodes", 1)))
+    for which, key, lr in ((0, "opt_pi", lr_pi), (1, "opt_v", lr_v)):
+        if key in kv:
+            tr.set_optimizer(which, OPT[kv[key]], lr)
     iters = int(kv["iters"])
     worst = {}
+    adam = {w: kv.get(k) == "adam" for w, k in ((0, "opt_pi"), (1, "opt_v"))}
+    lrs = {0: lr_pi, 1: lr_v}
+    mask = {0: None, 1: None}
+    nsteps = {0: 0, 1: 0}
     for it in range(iters):
         p = "it%d_" % it
         f = g[p + "step_choice"] if (forced and algo != po.OR_PG) else None
@@ -148,14 +156,23 @@ def run_oracle_against(name, forced=True):
         np.testing.assert_array_equal(tr.buf(po.BUF_ROW_IS_END), g[p + "row_is_end"])
         checks = [("advantages", tr.buf(po.BUF_ADVANTAGES), g[p + "advantages"]),
                   ("policy_grads", tr.buf(po.BUF_POLICY_GRADS),
-                   g[p + "policy_grads"].ravel()),
-                  ("policy_params", tr.params(0), g[p + "policy_params"])]
+                   g[p + "policy_grads"].ravel())]
         if algo != po.OR_PG:
             checks += [("values", tr.buf(po.BUF_VALUES), g[p + "values_before"]),
-                       ("value_grad", tr.buf(po.BUF_VALUE_GRAD), g[p + "value_grad"]),
-                       ("value_params", tr.params(1), g[p + "value_params"])]
+                       ("value_grad", tr.buf(po.BUF_VALUE_GRAD), g[p + "value_grad"])]
         for what, x, y in checks:
             worst[what] = max(worst.get(what, 0), assert_close(x, y, what=p + what))
+        params = [(0, "policy_params", "policy_grads")]
+        if algo != po.OR_PG:
+            params.append((1, "value_params", "value_grad"))
+        for w, what, gk in params:
+            gr = g[p + gk]
+            nsteps[w] += gr.reshape(-1, gr.shape[-1]).shape[0]
+            if adam[w]:
+                mask[w] = noise_mask(gr, mask[w])
+            worst[what] = max(worst.get(what, 0), assert_params_close(
+                tr.params(w), g[p + what], mask[w], 2 * lrs[w] * nsteps[w],
+                what=p + what))
         assert tr.rng == int(g[p + "x_end"][0])
     return worst
 
@@ -164,6 +181,27 @@ def run_oracle_against(name, forced=True):
 def test_learner_matches_reference(name):
     worst = run_oracle_against(name, forced=True)
     print(name, {k: "%.2e" % v for k, v in worst.items()})
+
+
+@pytest.mark.parametrize("name", ["ppo_adam_b8d2", "ac_mom_b8d2", "klppo_b8d2"])
+def test_optimizer_restatement_on_reference_gradients(name):
+    """or_opt_step fed the reference's own recorded gradients reproduces the
+    reference's parameters after every step (momentum / adam / sgd with weight
+    decay, state carried across learn() calls)."""
+    g = golden(name)
+    kv = parse_meta(g)
+    ac = kv["algo"] == "ac"
+    for w, pk, gk, ok, lr, wd in (
+            (0, "policy_params", "policy_grads", "opt_pi", 1e-5 if ac else 1e-4,
+             float(kv.get("wd_pi", 0))),
+            (1, "value_params", "value_grad", "opt_v", 1e-4 if ac else 1e-5, 0.0)):
+        p = np.array(g["init_policy" if w == 0 else "init_value"], np.float32)
+        opt = po.Opt(OPT[kv.get(ok, "sgd")], lr, wd)
+        for it in range(int(kv["iters"])):
+            gr = g["it%d_%s" % (it, gk)]
+            for row in gr.reshape(-1, gr.shape[-1]):
+                opt.step(p, row)
+            assert_close(p, g["it%d_%s" % (it, pk)], tol=1e-6, what=pk)
 
 
 @pytest.mark.parametrize("name", ["ppo_b8d2", "ac_b8d2", "pg_b8d1", "klppo_b8d2"])
