@@ -12,13 +12,13 @@ LIB_PATH = os.path.join(HERE, "libxylo_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "xylo_hip.h")
 
 XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)
-XH_PPO, XH_AC, XH_KLPPO = 0, 1, 2
+XH_PPO, XH_AC, XH_KLPPO, XH_PG = 0, 1, 2, 3
 HEURISTICS = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
 XH_POLICY, XH_VALUE = 0, 1
 OPTIMIZERS = {"sgd": 0, "momentum": 1, "adam": 2}
 (BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
  BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
- BUF_LOGITS, BUF_PROBS, BUF_V_STATE0, BUF_QOLD, BUF_KL) = range(17)
+ BUF_LOGITS, BUF_PROBS, BUF_V_STATE0, BUF_QOLD, BUF_KL, BUF_LEN) = range(18)
 
 
 class XhError(RuntimeError):

@@ -1,0 +1,265 @@
+// dense_kernels.hip -- full_layer (nn.h:60-110) forward / backward as one
+// f32 MFMA GEMM template for gfx950, plus the row-gathering loaders that let
+// a layer read observations straight from the int8 env states.
+//
+// C(m, n) = sum_k A(m, k) B(k, n), 64x64 output tile per 256-thread
+// workgroup (4 waves in a 2x2 grid of 32x32 v_mfma_f32_32x32x2_f32 tiles),
+// K staged through LDS in slices of 16 with a register prefetch of the next
+// slice.  The operand loaders and the epilogue are template functors:
+//   forward      Y = act(X W^T + b)           A = X rows, B = W^T
+//   data grad    dX = (dY W) * [H > 0]        A = dY, B = W, relu mask of H
+//   weight grad  [dW | db] = dY^T [X | 1]     A = dY^T, B = [X | 1], split-K
+//                                             over rows into per-split slabs
+// One dimension may be a device-side row count (rows of this learn() batch),
+// so a launch needs no host synchronisation.
+#include "xh_device.h"
+#include "xh_kernels.h"
+
+namespace xh {
+namespace dense {
+
+constexpr int BM = 64, BN = 64, BK = 16, PAD = 4;
+
+// ------------------------------------------------------------- loaders ----
+// Each loader returns element (i, k) of its operand viewed as [I x K]; for A
+// i = m, for B i = n.  kKContig: consecutive k are adjacent in memory (pick
+// the thread -> element order that coalesces).
+struct RowMajor {  // p[i * ld + k]
+  const float *p;
+  int ld;
+  static constexpr bool kKContig = true;
+  __device__ float operator()(int i, int k) const { return p[(size_t)i * ld + k]; }
+};
+struct ColMajor {  // p[k * ld + i]
+  const float *p;
+  int ld;
+  static constexpr bool kKContig = false;
+  __device__ float operator()(int i, int k) const { return p[(size_t)k * ld + i]; }
+};
+// [X | 1] as the B operand of a weight gradient: element (n, k=row) =
+// X[row][n] for n < ncol, 1 for n == ncol (the bias column).
+struct RowsOnes {
+  const float *p;
+  int ld, ncol;
+  static constexpr bool kKContig = false;
+  __device__ float operator()(int n, int r) const {
+    return n < ncol ? p[(size_t)r * ld + n] : 1.0f;
+  }
+};
+// observation::to_vector (bin_packing.h:31-40, generalised to D dims) of
+// row r: feature k = bin (k / 2D), c = k % 2D: c < D -> bins[bin][c] / 8,
+// else item[c - D] / 8.  Row r is slot s, env e with s * N + e = list[r]
+// (list == nullptr: slot `slot`, env r).
+struct ObsRows {
+  EnvDesc E;
+  const int8_t *bins, *items;
+  const int *list;
+  int N, slot;
+  __device__ float feature(int r, int k) const {
+    const int idx = list ? list[r] : slot * N + r;
+    const int D = E.D, bin = k / (2 * D), c = k - bin * 2 * D;
+    const int v = c < D ? bins[(size_t)idx * E.B * D + bin * D + c]
+                        : items[(size_t)idx * 4 + c - D];
+    return (float)v * (1.0f / (float)kCapacity);
+  }
+};
+struct ObsA : ObsRows {  // A operand: (m = row, k = feature)
+  static constexpr bool kKContig = true;
+  __device__ float operator()(int r, int k) const { return feature(r, k); }
+};
+struct ObsOnesB : ObsRows {  // B operand of dW1: (n = feature | 1, k = row)
+  int ncol;
+  static constexpr bool kKContig = false;
+  __device__ float operator()(int n, int r) const {
+    return n < ncol ? feature(r, n) : 1.0f;
+  }
+};
+
+// ----------------------------------------------------------- epilogues ----
+struct EpBiasAct {  // Y[m][n] = act(c + b[n])
+  float *y;
+  int ld;
+  const float *bias;
+  int relu;
+  __device__ void operator()(int m, int n, int, float c) const {
+    float v = c + bias[n];
+    if (relu) v = v > 0.0f ? v : 0.0f;
+    y[(size_t)m * ld + n] = v;
+  }
+};
+struct EpReluMask {  // dX[m][n] = H[m][n] > 0 ? c : 0 (relu backward, nn.h:364-376)
+  float *dx;
+  int ld;
+  const float *h;
+  __device__ void operator()(int m, int n, int, float c) const {
+    dx[(size_t)m * ld + n] = h[(size_t)m * ld + n] > 0.0f ? c : 0.0f;
+  }
+};
+struct EpSlab {  // weight-gradient slab: [A(out x in), b(out)] of one layer
+  float *slab;
+  int stride, oW, oB, in;
+  __device__ void operator()(int m, int n, int split, float c) const {
+    float *s = slab + (size_t)split * stride;
+    if (n < in)
+      s[oW + m * in + n] = c;
+    else
+      s[oB + m] = c;
+  }
+};
+
+// ---------------------------------------------------------------- GEMM ----
+// dyn: 0 = static sizes, 1 = M is *rows, 2 = K is *rows (each <= the static
+// bound).  Split-K: blockIdx.z takes K range [z*kper, (z+1)*kper).
+template <class LA, class LB, class EP>
+__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
+                                                   int N, int K, const int *rows,
+                                                   int dyn) {
+  __shared__ float As[BK][BM + PAD];
+  __shared__ float Bs[BK][BN + PAD];
+  if (dyn == 1) M = min(M, *rows);
+  if (dyn == 2) K = min(K, *rows);
+  const int bm = blockIdx.x * BM, bn = blockIdx.y * BN;
+  if (bm >= M && dyn == 1) return;  // no rows for this tile (uniform exit)
+  const int splits = gridDim.z;
+  int kper = (K + splits - 1) / splits;
+  kper = (kper + BK - 1) / BK * BK;
+  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
+  f32x16 acc = zero16();
+
+  // this thread's 4 (i, kk) positions in a BM x BK (or BN x BK) slice
+  auto pos = [&](bool kcontig, int j, int &i, int &kk) {
+    if (kcontig) {
+      kk = tid & (BK - 1);
+      i = (tid >> 4) + 16 * j;
+    } else {
+      i = tid & 63;
+      kk = (tid >> 6) + 4 * j;
+    }
+  };
+  float ra[4], rb[4];
+  auto fetch = [&](int kb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int i, kk;
+      pos(LA::kKContig, j, i, kk);
+      const int m = bm + i, k = kb + kk;
+      ra[j] = (m < M && k < k1) ? la(m, k) : 0.0f;
+      pos(LB::kKContig, j, i, kk);
+      const int n = bn + i;
+      rb[j] = (n < N && kb + kk < k1) ? lb(n, kb + kk) : 0.0f;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int i, kk;
+      pos(LA::kKContig, j, i, kk);
+      As[kk][i] = ra[j];
+      pos(LB::kKContig, j, i, kk);
+      Bs[kk][i] = rb[j];
+    }
+  };
+
+  if (k0 < k1) fetch(k0);
+  for (int kb = k0; kb < k1; kb += BK) {
+    __syncthreads();
+    stash();
+    __syncthreads();
+    if (kb + BK < k1) fetch(kb + BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2)
+      acc = mfma32(As[kk + h][wm * 32 + lr], Bs[kk + h][wn * 32 + lr], acc);
+  }
+  const int n = bn + wn * 32 + lr;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = bm + wm * 32 + acc_row(r, h);
+    if (m < M && n < N) ep(m, n, blockIdx.z, acc[r]);
+  }
+}
+
+template <class LA, class LB, class EP>
+hipError_t gemm(LA la, LB lb, EP ep, int M, int N, int K, const int *rows,
+                int dyn, int splits, hipStream_t s) {
+  dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits < 1 ? 1 : splits);
+  hipLaunchKernelGGL((gemm_kernel<LA, LB, EP>), grid, dim3(256), 0, s, la, lb,
+                     ep, M, N, K, rows, dyn);
+  return hipGetLastError();
+}
+
+}  // namespace dense
+
+// ----------------------------------------------------- full-MLP policy ----
+// Layer l of a full MLP whose flat parameters follow model::parameters()
+// (nn.h:499-508): widths w[0] = input, ..., w[L] = output.
+static int layer_offset(const int *w, int l) {
+  int off = 0;
+  for (int i = 0; i < l; ++i) off += w[i + 1] * w[i] + w[i + 1];
+  return off;
+}
+
+hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
+  using namespace dense;
+  hipError_t e = hipSuccess;
+  for (int l = 0; l < a.nlayers && e == hipSuccess; ++l) {
+    const int in = a.w[l], out = a.w[l + 1];
+    const float *W = a.params + layer_offset(a.w, l);
+    EpBiasAct ep{a.act[l], out, W + out * in, l + 1 < a.nlayers};
+    RowMajor wt{W, in};  // B(n = out unit, k) = W[n][k]
+    if (l == 0) {
+      ObsA la;
+      la.E = a.env;
+      la.bins = a.bins;
+      la.items = a.items;
+      la.list = a.list;
+      la.N = a.N;
+      la.slot = a.slot;
+      e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
+    } else {
+      RowMajor la{a.act[l - 1], in};
+      e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
+    }
+  }
+  return e;
+}
+
+hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
+                        hipStream_t s) {
+  using namespace dense;
+  hipError_t e = hipSuccess;
+  for (int l = a.nlayers - 1; l >= 0 && e == hipSuccess; --l) {
+    const int in = a.w[l], out = a.w[l + 1];
+    const int off = layer_offset(a.w, l);
+    // [dW | db] = dY^T [X | 1] over the batch rows (nn.h:81-100)
+    ColMajor dyT{a.grad[l], out};  // A(m = out unit, k = row) = dY[row][m]
+    EpSlab es{slab, stride, off, off + out * in, in};
+    if (l == 0) {
+      ObsOnesB lb;
+      lb.E = a.env;
+      lb.bins = a.bins;
+      lb.items = a.items;
+      lb.list = a.list;
+      lb.N = a.N;
+      lb.slot = a.slot;
+      lb.ncol = in;
+      e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
+               splits, s);
+    } else {
+      RowsOnes lb{a.act[l - 1], in, in};
+      e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
+               splits, s);
+      if (e != hipSuccess) break;
+      // dX = (dY W) * relu'(X); layer 0 gets no backward (nn.h:516-526)
+      RowMajor dy{a.grad[l], out};              // A(m = row, k = out unit)
+      ColMajor wn{a.params + off, in};          // B(n = in unit, k) = W[k][n]
+      EpReluMask em{a.grad[l - 1], in, a.act[l - 1]};
+      e = gemm(dy, wn, em, a.max_rows, in, out, a.rows, a.rows ? 1 : 0, 1, s);
+    }
+  }
+  return e;
+}
+
+}  // namespace xh

@@ -156,6 +156,62 @@ struct HeuristicArgs {
   int *trace;
   long trace_cap;
 };
+// Full MLP (full_layer / relu chain, nn.h:60-110, 350-377) over a batch of
+// rows whose input is the observation of (slot, env) states
+// (dense_kernels.hip).  Layer l maps w[l] -> w[l+1]; relu after every layer
+// but the last.  act[l] / grad[l]: [max_rows][w[l+1]] outputs and
+// dL/d(pre-activation) of layer l.
+struct MlpArgs {
+  EnvDesc env;
+  const int8_t *bins, *items;  // Batch state layout
+  const int *list;             // row -> slot * N + env (nullptr: env = row)
+  int N, slot;                 // slot used when list == nullptr
+  const int *rows;             // device row count (nullptr: max_rows)
+  int max_rows;
+  int nlayers;
+  int w[4];
+  const float *params;  // flat model::parameters() layout
+  float *act[3];
+  float *grad[3];
+};
+hipError_t mlp_forward(const MlpArgs &a, hipStream_t s);
+// Weight gradients of every layer into slab[split] (flat layout), data
+// gradients down to layer 1 (layer 0 gets no backward, nn.h:516-526).
+hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
+                        hipStream_t s);
+
+// REINFORCE (pg_kernels.hip).  Batch.T = the per-iteration step bound.
+struct PgStepArgs {
+  EnvDesc env;
+  Batch b;
+  int t, episodes;
+  const float *logits;    // [N][B] of slot t
+  const int32_t *forced;  // [T][N] or nullptr
+  int *ep_done, *len, *active;
+};
+struct PgLearnArgs {
+  int N, B, episodes;
+  float gamma;
+  const int *len;
+  int *row_off, *list, *nrows;
+  const uint8_t *done;
+  const int32_t *action;
+  float *rtg;       // [rows]
+  double *ep_part;  // [N]
+  double *stats;    // [2]: sum of slot-0 returns, trajectories
+  const float *logits;
+  float *dlogits;
+  float *adv_grid;  // [T][N] advantages for introspection
+};
+hipError_t launch_pg_env_init(const EnvDesc &env, Batch b, uint32_t x0,
+                              int env_offset, uint64_t stride, hipStream_t s);
+hipError_t launch_pg_begin(int N, int *active, int *ep_done, int *len,
+                           hipStream_t s);
+hipError_t launch_pg_step(const PgStepArgs &a, hipStream_t s);
+hipError_t launch_pg_rows(const PgLearnArgs &a, hipStream_t s);
+hipError_t launch_pg_adv(const PgLearnArgs &a, hipStream_t s);
+hipError_t launch_pg_loss(const PgLearnArgs &a, int max_rows, hipStream_t s);
+
 bool heuristic_shape_supported(int B, int D);
 hipError_t launch_heuristic(const HeuristicArgs &a, int kind, hipStream_t s);
 

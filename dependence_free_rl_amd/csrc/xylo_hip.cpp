@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -140,6 +141,19 @@ struct xh_trainer {
     float t = 1.0f;                    // adam_optimizer::t (nn.h:694)
     float *m = nullptr, *v = nullptr;  // velocity / moments (device)
   } opt[2];
+  // REINFORCE (XH_PG): full-MLP policy buffers and episode bookkeeping
+  struct pg_state {
+    int nlayers = 0, w[4] = {0, 0, 0, 0};
+    float *act[3] = {nullptr, nullptr, nullptr};
+    float *grad[3] = {nullptr, nullptr, nullptr};
+    int *ep_done = nullptr, *len = nullptr, *active = nullptr;
+    int *row_off = nullptr, *list = nullptr, *nrows = nullptr;
+    float *rtg = nullptr;
+    double *ep_part = nullptr, *stats = nullptr;
+    int *host_active = nullptr;  // pinned
+    int slot_end = 0;            // slot holding the envs' current states
+  } pg;
+  int Tb = 0;  // Batch steps: cfg.steps, or REINFORCE's per-iteration bound
   uint32_t jump_mul = 1;
   int rgrid = 0;
   bool need_shift = false;
@@ -152,7 +166,7 @@ struct xh_trainer {
   xh::Batch batch() const {
     xh::Batch b;
     b.N = cfg.num_envs;
-    b.T = cfg.steps;
+    b.T = Tb;
     b.bins = bins;
     b.items = items;
     b.action = action;
@@ -178,7 +192,7 @@ struct xh_trainer {
     return a;
   }
   size_t N() const { return (size_t)cfg.num_envs; }
-  size_t T() const { return (size_t)cfg.steps; }
+  size_t T() const { return (size_t)Tb; }
   size_t BD() const { return (size_t)cfg.bins * cfg.dims; }
 };
 
@@ -255,6 +269,7 @@ size_t buffer_bytes(const xh_trainer *t, int which) {
     case XH_BUF_PROBS: return N * t->cfg.bins * 4;
     case XH_BUF_QOLD: return t->qold ? T * N * t->cfg.bins * 4 : 0;
     case XH_BUF_KL: return t->kl_log ? (size_t)t->cfg.epochs * 12 : 0;
+    case XH_BUF_LEN: return t->pg.len ? N * 4 : 0;
   }
   return 0;
 }
@@ -278,6 +293,7 @@ void *buffer_ptr(const xh_trainer *t, int which) {
     case XH_BUF_POLICY_GRADS: return t->pgrads;
     case XH_BUF_LOGITS: return t->logits;
     case XH_BUF_PROBS: return t->probs;
+    case XH_BUF_LEN: return t->pg.len;
   }
   return nullptr;
 }
@@ -384,8 +400,8 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
     float ms = 0.0f;
     if (st == XH_OK && hipEventElapsedTime(&ms, ev0, ev1) == hipSuccess)
       e->elapsed_ms = ms;
-    hipEventDestroy(ev0);
-    hipEventDestroy(ev1);
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
   }
   return st;
 }
@@ -417,7 +433,11 @@ int refresh_value_transpose(xh_trainer *t) {
   });
 }
 
+int do_pg_rollout(xh_trainer *t);
+int do_pg_learn(xh_trainer *t);
+
 int do_rollout(xh_trainer *t) {
+  if (t->cfg.algo == XH_PG) return do_pg_rollout(t);
   hipStream_t s = t->ctx->stream;
   const size_t N = t->N(), T = t->T();
   if (t->need_shift) {  // replay_buffer::forget(): open trajectories continue
@@ -448,6 +468,7 @@ int do_rollout(xh_trainer *t) {
 }
 
 int do_learn(xh_trainer *t) {
+  if (t->cfg.algo == XH_PG) return do_pg_learn(t);
   hipStream_t s = t->ctx->stream;
   const xh_config &c = t->cfg;
   xh::ValueArgs va = t->vargs();
@@ -537,6 +558,230 @@ int do_learn(xh_trainer *t) {
   return XH_OK;
 }
 
+// ------------------------------------------------------------ REINFORCE ----
+// policy_gradient_learner (policy_gradient.h:88-147) with a full-MLP
+// softmax-xent policy (pg_training.cc:10-20), each env playing cfg.steps
+// whole episodes per iteration.
+
+// Upper bound of an episode's length: every non-final step puts an item into
+// a bin, and a bin takes at most min_d floor(8 / smallest item extent in d)
+// items before some extent would go negative.
+int pg_episode_bound(const xh::EnvDesc &E) {
+  int per_bin = 8;  // capacity per dim (bin_packing.h:48)
+  for (int d = 0; d < E.D; ++d) {
+    const int m = std::min(E.item_a[d], E.item_b[d]);
+    per_bin = std::min(per_bin, 8 / m);
+  }
+  return E.B * per_bin + 1;
+}
+
+xh::MlpArgs pg_mlp(const xh_trainer *t, bool learn, int slot) {
+  xh::MlpArgs m{};
+  m.env = t->env;
+  m.bins = t->bins;
+  m.items = t->items;
+  m.N = (int)t->N();
+  m.nlayers = t->pg.nlayers;
+  for (int i = 0; i < 4; ++i) m.w[i] = t->pg.w[i];
+  m.params = t->pp;
+  for (int i = 0; i < 3; ++i) {
+    m.act[i] = t->pg.act[i];
+    m.grad[i] = t->pg.grad[i];
+  }
+  if (learn) {
+    m.list = t->pg.list;
+    m.rows = t->pg.nrows;
+    m.max_rows = (int)(t->T() * t->N());
+  } else {
+    m.slot = slot;
+    m.max_rows = (int)t->N();
+  }
+  return m;
+}
+
+int create_pg(xh_ctx *ctx, const xh_config &c, xh_trainer **out) {
+  if (c.bins < 2 || c.bins > 128 || c.dims < 1 || c.dims > 3)
+    return fail(XH_ERR_INVALID, "REINFORCE: bins %d (2..128), dims %d (1..3)",
+                c.bins, c.dims);
+  if (c.policy_h1 < 1 || c.policy_h2 < 0 || c.policy_h1 > 1024 ||
+      c.policy_h2 > 1024)
+    return fail(XH_ERR_INVALID, "REINFORCE: widths [%d,%d]", c.policy_h1,
+                c.policy_h2);
+  if (c.steps < 1 || c.steps > 64)
+    return fail(XH_ERR_INVALID, "REINFORCE: episodes per env %d not in [1,64]",
+                c.steps);
+  if (c.num_envs < 1 || c.num_envs_global < c.num_envs || c.env_offset < 0 ||
+      c.env_offset + c.num_envs > c.num_envs_global)
+    return fail(XH_ERR_INVALID, "env partition offset %d + %d > global %d",
+                c.env_offset, c.num_envs, c.num_envs_global);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto *t = new xh_trainer;
+  t->ctx = ctx;
+  t->cfg = c;
+  t->cfg.epochs = 1;
+  t->cfg.rng_state = c.rng_state % 2147483647u;
+  if (t->cfg.rng_state == 0) t->cfg.rng_state = 1;
+  t->env = make_env(c.bins, c.dims);
+  t->Tb = c.steps * pg_episode_bound(t->env);
+  auto &pg = t->pg;
+  pg.w[0] = c.bins * 2 * c.dims;
+  pg.w[1] = c.policy_h1;
+  pg.nlayers = 2;
+  if (c.policy_h2 > 0) {
+    pg.w[2] = c.policy_h2;
+    pg.nlayers = 3;
+  }
+  pg.w[pg.nlayers] = c.bins;
+  t->np = 0;
+  for (int l = 0; l < pg.nlayers; ++l) t->np += pg.w[l + 1] * pg.w[l] + pg.w[l + 1];
+  t->nv = 0;
+  const size_t N = t->N(), T = t->T(), R = T * N;
+  int st = XH_OK;
+  auto A = [&](auto **p, size_t bytes) {
+    if (st == XH_OK) st = dalloc(t, p, bytes);
+  };
+  A(&t->bins, (T + 1) * N * t->BD());
+  A(&t->items, (T + 1) * N * 4);
+  A(&t->action, T * N * 4);
+  A(&t->forced, T * N * 4);
+  A(&t->pold, T * N * 4);
+  A(&t->done, T * N);
+  A(&t->rng, N * 4);
+  A(&t->pp, (size_t)t->np * 4);
+  A(&t->adv, T * N * 4);
+  for (int l = 0; l < pg.nlayers; ++l) {
+    A(&pg.act[l], R * pg.w[l + 1] * 4);
+    A(&pg.grad[l], R * pg.w[l + 1] * 4);
+  }
+  A(&pg.ep_done, N * 4);
+  A(&pg.len, N * 4);
+  A(&pg.active, 4);
+  A(&pg.row_off, N * 4);
+  A(&pg.list, R * 4);
+  A(&pg.nrows, 4);
+  A(&pg.rtg, R * 4);
+  A(&pg.ep_part, N * 8);
+  A(&pg.stats, 2 * 8);
+  t->pslab_n = 64;
+  t->pslab_stride = (t->np + 63) & ~63;
+  A(&t->pslab, (size_t)t->pslab_n * t->pslab_stride * 4);
+  A(&t->pgrads, (size_t)t->np * 4);
+  A(&t->logits, N * c.bins * 4);
+  A(&t->probs, N * c.bins * 4);
+  if (st == XH_OK && hipHostMalloc((void **)&pg.host_active, 4) != hipSuccess)
+    st = fail(XH_ERR_HIP, "hipHostMalloc");
+  t->opt[XH_POLICY].lr = c.lr_policy;
+  t->opt[XH_POLICY].wd = c.wd_policy;
+  hipError_t e = hipSuccess;
+  if (st == XH_OK) {
+    e = xh::launch_pg_env_init(t->env, t->batch(), t->cfg.rng_state,
+                               c.env_offset, kEvalStride, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) st = fail(XH_ERR_HIP, "env init: %s", hipGetErrorString(e));
+  }
+  t->counted = true;
+  ++ctx->trainers;
+  if (st != XH_OK) {
+    std::string keep = g_err;
+    xh_trainer_destroy(t);
+    g_err = keep;
+    return st;
+  }
+  *out = t;
+  return XH_OK;
+}
+
+// agent::play_one_episode x cfg.steps for every env (rl.h:325-354): one
+// forward + one step kernel per env step, until every env has finished its
+// episodes (checked every 8 steps through a pinned flag).
+int do_pg_rollout(xh_trainer *t) {
+  hipStream_t s = t->ctx->stream;
+  const size_t N = t->N();
+  auto &pg = t->pg;
+  if (t->need_shift) {  // the envs' current states -> slot 0
+    HIPCHK(hipMemcpyAsync(t->bins, t->bins + (size_t)pg.slot_end * N * t->BD(),
+                          N * t->BD(), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(t->items, t->items + (size_t)pg.slot_end * N * 4,
+                          N * 4, hipMemcpyDeviceToDevice, s));
+    t->need_shift = false;
+  }
+  CHK(timed(t, "rollout_step", [&]() {
+    return xh::launch_pg_begin((int)N, pg.active, pg.ep_done, pg.len, s);
+  }));
+  xh::PgStepArgs a{};
+  a.env = t->env;
+  a.b = t->batch();
+  a.episodes = t->cfg.steps;
+  a.logits = pg.act[pg.nlayers - 1];
+  a.forced = t->use_forced ? t->forced : nullptr;
+  a.ep_done = pg.ep_done;
+  a.len = pg.len;
+  a.active = pg.active;
+  int steps = 0;
+  for (int step = 0; step < t->Tb; ++step) {
+    xh::MlpArgs m = pg_mlp(t, false, step);
+    CHK(timed(t, "rollout_step", [&]() { return xh::mlp_forward(m, s); }));
+    a.t = step;
+    CHK(timed(t, "rollout_step", [&]() { return xh::launch_pg_step(a, s); }));
+    steps = step + 1;
+    if (steps % 8 == 0 || steps == t->Tb) {
+      HIPCHK(hipMemcpyAsync(pg.host_active, pg.active, 4,
+                            hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (*pg.host_active == 0) break;
+    }
+  }
+  if (*pg.host_active != 0)
+    return fail(XH_ERR_STATE, "REINFORCE rollout: %d envs still playing after "
+                "the step bound %d", *pg.host_active, t->Tb);
+  pg.slot_end = steps;
+  return XH_OK;
+}
+
+// policy_gradient_learner::learn (policy_gradient.h:95-123): rows = every
+// transition in replay-buffer order, advantages = reversed rewards-to-go minus
+// the mean trajectory return, one optimizer step on policy_loss.
+int do_pg_learn(xh_trainer *t) {
+  hipStream_t s = t->ctx->stream;
+  auto &pg = t->pg;
+  xh::PgLearnArgs L{};
+  L.N = (int)t->N();
+  L.B = t->cfg.bins;
+  L.episodes = t->cfg.steps;
+  L.gamma = t->cfg.gamma;
+  L.len = pg.len;
+  L.row_off = pg.row_off;
+  L.list = pg.list;
+  L.nrows = pg.nrows;
+  L.done = t->done;
+  L.action = t->action;
+  L.rtg = pg.rtg;
+  L.ep_part = pg.ep_part;
+  L.stats = pg.stats;
+  L.logits = pg.act[pg.nlayers - 1];
+  L.dlogits = pg.grad[pg.nlayers - 1];
+  L.adv_grid = t->adv;
+  CHK(timed(t, "policy_train", [&]() { return xh::launch_pg_rows(L, s); }));
+  CHK(timed(t, "policy_train", [&]() { return xh::launch_pg_adv(L, s); }));
+  CHK(allreduce_d(t, pg.stats, 2));  // baseline over the job's trajectories
+  const xh::MlpArgs m = pg_mlp(t, true, 0);
+  CHK(timed(t, "policy_train", [&]() { return xh::mlp_forward(m, s); }));
+  CHK(timed(t, "policy_train", [&]() {
+    return xh::launch_pg_loss(L, m.max_rows, s);
+  }));
+  CHK(timed(t, "policy_train", [&]() {
+    return xh::mlp_backward(m, t->pslab, t->pslab_stride, t->pslab_n, s);
+  }));
+  CHK(timed(t, "reduce_sgd", [&]() {
+    return xh::launch_slab_reduce(t->pslab, t->pslab_n, t->pslab_stride, t->np,
+                                  t->pgrads, s);
+  }));
+  CHK(allreduce(t, t->pgrads, t->np));
+  CHK(opt_apply(t, XH_POLICY, t->pp, t->pgrads, t->np));
+  t->need_shift = true;
+  return XH_OK;
+}
+
 }  // namespace
 
 // ================================================================= C ABI ==
@@ -585,7 +830,7 @@ int xh_ctx_create(int device, int rank, int world, const void *uid128,
     }
     if (world > 1) {
       if (!uid128) {
-        hipStreamDestroy(c->stream);
+        (void)hipStreamDestroy(c->stream);
         delete c;
         return fail(XH_ERR_INVALID, "world > 1 needs the RCCL unique id");
       }
@@ -593,7 +838,7 @@ int xh_ctx_create(int device, int rank, int world, const void *uid128,
       std::memcpy(&id, uid128, sizeof id);
       ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
       if (r != ncclSuccess) {
-        hipStreamDestroy(c->stream);
+        (void)hipStreamDestroy(c->stream);
         delete c;
         return fail(XH_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
       }
@@ -661,6 +906,13 @@ void xh_config_default(xh_config *c, int algo, int bins, int dims, int num_envs,
   c->lr_policy = algo == XH_AC ? 1e-5f : 1e-4f;
   c->lr_value = algo == XH_AC ? 1e-4f : 1e-5f;
   if (algo == XH_KLPPO) c->wd_policy = 1e-5f;  // ppo2_training.cc:20
+  if (algo == XH_PG) {  // pg_training.cc:10-20: full 4B->256->128->B, 1e-4
+    c->policy_h1 = 256;
+    c->policy_h2 = 128;
+    c->epochs = 1;
+    c->lr_policy = 1e-4f;
+    c->lr_value = 0.0f;
+  }
   c->gamma = 0.99f;
   c->lambda = 0.95f;
   c->clip_eps = 0.2f;
@@ -673,6 +925,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
   return guard([&]() -> int {
     if (!ctx || !cfg || !out) return fail(XH_ERR_INVALID, "null arg");
     const xh_config &c = *cfg;
+    if (c.algo == XH_PG) return create_pg(ctx, c, out);
     if (c.algo != XH_PPO && c.algo != XH_AC && c.algo != XH_KLPPO)
       return fail(XH_ERR_INVALID, "algo %d", c.algo);
     if (c.algo == XH_KLPPO && c.bins > 64)
@@ -704,6 +957,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     auto *t = new xh_trainer;
     t->ctx = ctx;
     t->cfg = c;
+    t->Tb = c.steps;
     // minstd_rand0 seeding rule: s mod m, 0 -> 1
     t->cfg.rng_state = c.rng_state % 2147483647u;
     if (t->cfg.rng_state == 0) t->cfg.rng_state = 1;
@@ -800,13 +1054,14 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
 int xh_trainer_destroy(xh_trainer *t) {
   return guard([&]() -> int {
     if (!t) return XH_OK;
-    hipSetDevice(t->ctx->device);
-    hipStreamSynchronize(t->ctx->stream);
+    (void)hipSetDevice(t->ctx->device);
+    (void)hipStreamSynchronize(t->ctx->stream);
     for (auto &ev : t->events) {
-      hipEventDestroy(ev.start);
-      hipEventDestroy(ev.stop);
+      (void)hipEventDestroy(ev.start);
+      (void)hipEventDestroy(ev.stop);
     }
     for (void *p : t->allocs) (void)hipFree(p);
+    if (t->pg.host_active) (void)hipHostFree(t->pg.host_active);
     xh_ctx *c = t->ctx;
     const bool counted = t->counted;
     delete t;
@@ -937,13 +1192,13 @@ int xh_trainer_set_forced_actions(xh_trainer *t, const int32_t *host) {
 }
 
 size_t xh_trainer_buffer_bytes(const xh_trainer *t, int which) {
-  return t ? buffer_bytes(t, which) : 0;
+  return t && buffer_ptr(t, which) ? buffer_bytes(t, which) : 0;
 }
 
 int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes) {
   return guard([&]() -> int {
     if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
-    const size_t want = buffer_bytes(t, which);
+    const size_t want = xh_trainer_buffer_bytes(t, which);
     if (!want || bytes != want)
       return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
                   bytes, want);
@@ -959,7 +1214,7 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
                           size_t bytes) {
   return guard([&]() -> int {
     if (!t || !host) return fail(XH_ERR_INVALID, "null arg");
-    const size_t want = buffer_bytes(t, which);
+    const size_t want = xh_trainer_buffer_bytes(t, which);
     if (!want || bytes != want)
       return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
                   bytes, want);
@@ -1060,8 +1315,8 @@ int xh_trainer_reset_timing(xh_trainer *t) {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     for (auto &ev : t->events) {
-      hipEventDestroy(ev.start);
-      hipEventDestroy(ev.stop);
+      (void)hipEventDestroy(ev.start);
+      (void)hipEventDestroy(ev.stop);
     }
     t->events.clear();
     return XH_OK;

@@ -18,13 +18,13 @@ import numpy as np
 
 from . import _lib
 from ._lib import (BUF_ACTION, BUF_ADV, BUF_BINS, BUF_DONE, BUF_ITEMS,
-                   BUF_KL, BUF_LOGITS, BUF_POLD, BUF_POLICY_GRADS, BUF_PROBS,
+                   BUF_KL, BUF_LEN, BUF_LOGITS, BUF_POLD, BUF_POLICY_GRADS, BUF_PROBS,
                    BUF_QOLD, BUF_RNG, BUF_TARGETS, BUF_V_STATE, BUF_V_STATE0,
-                   BUF_V_TERM, BUF_VALUE_GRAD, XH_AC, XH_KLPPO, XH_POLICY,
-                   XH_PPO, XH_VALUE, check)
+                   BUF_V_TERM, BUF_VALUE_GRAD, XH_AC, XH_KLPPO, XH_PG,
+                   XH_POLICY, XH_PPO, XH_VALUE, check)
 
 POLICY, VALUE = XH_POLICY, XH_VALUE
-ALGOS = {"ppo": XH_PPO, "ac": XH_AC, "klppo": XH_KLPPO}
+ALGOS = {"ppo": XH_PPO, "ac": XH_AC, "klppo": XH_KLPPO, "pg": XH_PG}
 
 
 def _ptr(a):
@@ -139,6 +139,18 @@ def init_policy(dims, h1, h2, seed=0):
     return np.concatenate(parts).astype(np.float32)
 
 
+def init_full_policy(bins, dims, widths, seed=0):
+    """REINFORCE's full-layer policy 4B -> widths... -> B, full_layer init
+    N(0, 0.01) (nn.h:12-14,68), biases 0."""
+    rng = np.random.default_rng(seed)
+    sizes = [bins * 2 * dims] + [w for w in widths if w] + [bins]
+    parts = []
+    for fi, fo in zip(sizes[:-1], sizes[1:]):
+        parts.append(rng.normal(0.0, 0.01, fo * fi))
+        parts.append(np.zeros(fo))
+    return np.concatenate(parts).astype(np.float32)
+
+
 def init_value(bins, dims, v1=64, v2=32, seed=1):
     """full_layer init N(0, 0.01) (normal_initialize, nn.h:12-14,68)."""
     rng = np.random.default_rng(seed)
@@ -187,6 +199,10 @@ class Trainer:
         check(_lib.lib.xh_trainer_create(ctx.h, C.byref(cfg), C.byref(self.h)))
         self.np_ = _lib.lib.xh_trainer_num_params(self.h, POLICY)
         self.nv = _lib.lib.xh_trainer_num_params(self.h, VALUE)
+        if algo == "pg":  # steps = episodes per env; the batch has a step bound
+            self.episodes = steps
+            self.T = _lib.lib.xh_trainer_buffer_bytes(self.h, BUF_ACTION) // (
+                4 * num_envs)
 
     # ------------------------------------------------------------ params --
     def num_params(self, which):
@@ -249,6 +265,7 @@ class Trainer:
             BUF_PROBS: (np.float32, (N, B)),
             BUF_QOLD: (np.float32, (T, N, B)),
             BUF_KL: (np.float32, (self.epochs, 3)),
+            BUF_LEN: (np.int32, (N,)),
         }[which]
 
     def buffer(self, which):

@@ -61,10 +61,21 @@ int xh_ctx_allreduce_host(xh_ctx *ctx, float *data, size_t n);
  * PPO's k = 4 full-batch epochs with kl_regulated_loss and an adaptive beta
  * that carries over from one learn() to the next.  Per-bin shapes with
  * bins <= 64. */
-enum { XH_PPO = 0, XH_AC = 1, XH_KLPPO = 2 };
+/* XH_PG: policy_gradient_learner = REINFORCE (policy_gradient.h:88-147,
+ * bp::pg_learner, pg_training.cc) with a FULL-layer policy
+ * full(4B, policy_h1) - relu [- full(policy_h1, policy_h2) - relu] -
+ * full(., B) - softmax_cross_entropy (policy_h2 = 0: one hidden layer), no
+ * value net.  `steps` is the number of whole episodes each env plays per
+ * iteration (play_one_episode, rl.h:351-354); env g plays on its own engine
+ * stream, rng_state advanced by g * 2^26 draws (env 0 = the single-env
+ * reference run).  The batch buffers hold `xh_trainer_buffer_bytes`-sized
+ * [Tmax][N] grids, Tmax = steps * (longest possible episode); XH_BUF_LEN
+ * gives each env's step count of the last rollout. */
+enum { XH_PPO = 0, XH_AC = 1, XH_KLPPO = 2, XH_PG = 3 };
 
 typedef struct {
-  int algo;            /* XH_PPO | XH_AC (actor_critic_learner) | XH_KLPPO */
+  int algo;            /* XH_PPO | XH_AC (actor_critic_learner) | XH_KLPPO
+                          | XH_PG */
   int num_envs;        /* envs on this rank (multiple of 64/bins)            */
   int num_envs_global; /* envs in the whole job (reference-order RNG streams) */
   int env_offset;      /* global index of this rank's first env              */
@@ -143,6 +154,7 @@ enum {
   XH_BUF_QOLD = 15,    /* f32   [T][N][B] KL-PPO: sampled distributions      */
   XH_BUF_KL = 16,      /* f32   [epochs][3] KL-PPO: beta used, mean KL, new
                                   beta of the last learn()                   */
+  XH_BUF_LEN = 17,     /* int32 [N]  REINFORCE: env steps of the last rollout */
   XH_BUF_COUNT
 };
 size_t xh_trainer_buffer_bytes(const xh_trainer *t, int which);

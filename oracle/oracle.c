@@ -448,7 +448,8 @@ struct or_trainer {
   float gamma, lambda;
   float beta, d_targ; /* kl_ppo_learner (policy_gradient.h:332-333) */
   or_opt opt[2];      /* policy, value optimizers */
-  uint32_t x;
+  uint32_t x, x0;
+  uint32_t *xs;       /* per-env streams (or_trainer_set_env_streams) */
   /* workers */
   int32_t *bins, *item; /* N*B*D, N*D */
   int *steps;
@@ -524,7 +525,7 @@ or_trainer *or_trainer_create(int algo, const or_env_cfg *env, int N, int T,
   t->opt[1].wd = wd_v;
   t->beta = 1.0f;
   t->d_targ = 1e-9f;
-  t->x = x0;
+  t->x = t->x0 = x0;
   const int BD = env->B * env->D;
   t->bins = (int32_t *)malloc(sizeof(int32_t) * (size_t)N * BD);
   t->item = (int32_t *)calloc((size_t)N * 3, sizeof(int32_t));
@@ -561,6 +562,7 @@ void or_trainer_destroy(or_trainer *t) {
   free(t->item);
   free(t->steps);
   free(t->cur);
+  free(t->xs);
   or_opt_free(&t->opt[0]);
   or_opt_free(&t->opt[1]);
   free(t);
@@ -579,6 +581,26 @@ void or_trainer_set_optimizer(or_trainer *t, int which, int kind, float lr,
 }
 
 uint32_t or_trainer_rng(const or_trainer *t) { return t->x; }
+
+/* Independent per-env streams: env i draws from x0 advanced by i * stride
+ * (the device evaluators' and REINFORCE trainer's convention; env 0 is the
+ * single-env reference run).  Re-constructs the envs (2 draws each). */
+void or_trainer_set_env_streams(or_trainer *t, uint64_t stride) {
+  const int BD = t->env.B * t->env.D;
+  free(t->xs);
+  t->xs = (uint32_t *)malloc(sizeof(uint32_t) * t->N);
+  for (int i = 0; i < t->N; ++i) {
+    t->xs[i] = or_minstd_jump(t->x0, (uint64_t)i * stride);
+    or_env_construct(&t->env, t->bins + (size_t)i * BD,
+                     t->item + (size_t)i * 3, &t->xs[i]);
+  }
+}
+
+const uint32_t *or_trainer_env_streams(const or_trainer *t) { return t->xs; }
+
+static uint32_t *env_rng(or_trainer *t, int i) {
+  return t->xs ? &t->xs[i] : &t->x;
+}
 
 void or_trainer_get_params(const or_trainer *t, int which, float *out) {
   if (which == 0)
@@ -646,10 +668,10 @@ static int agent_step(or_trainer *t, int i, int forced_choice) {
   free(obs);
   int choice;
   if (forced_choice >= 0) {
-    (void)or_canonical(&t->x); /* the sampler's 2 engine draws */
+    (void)or_canonical(env_rng(t, i)); /* the sampler's 2 engine draws */
     choice = forced_choice;
   } else {
-    choice = or_discrete(&t->x, probs, B);
+    choice = or_discrete(env_rng(t, i), probs, B);
   }
 
   /* step log: state before apply (== prev, see rl.h:332-334) */
@@ -659,7 +681,7 @@ static int agent_step(or_trainer *t, int i, int forced_choice) {
   buf_append(&t->buf[OR_BUF_STEP_CHOICE], &choice, 1, sizeof(int32_t));
   buf_append(&t->buf[OR_BUF_STEP_PCHOICE], probs + choice, 1, sizeof(float));
 
-  or_env_apply(c, bins, item, choice, &t->x);
+  or_env_apply(c, bins, item, choice, env_rng(t, i));
   t->steps[i]++;
   st_t curr = st_copy(t, bins, item, i, t->steps[i]);
   const int over = or_env_game_over(c, curr.bins);
@@ -673,7 +695,7 @@ static int agent_step(or_trainer *t, int i, int forced_choice) {
   done32 = over;
   buf_append(&t->buf[OR_BUF_STEP_DONE], &done32, 1, sizeof(int32_t));
   if (over) {
-    or_env_reset(c, bins, item, &t->x);
+    or_env_reset(c, bins, item, env_rng(t, i));
     tj->frozen = 1;
     t->cur[i] = -1;
     return 0;

@@ -237,6 +237,19 @@ class Trainer:
                                                C.c_float]
         l.or_trainer_set_optimizer(self.h, which, kind, lr, wd, beta1, beta2)
 
+    def set_env_streams(self, stride=1 << 26):
+        """Env i on its own stream: x0 advanced by i * stride."""
+        l = lib()
+        l.or_trainer_set_env_streams.argtypes = [C.c_void_p, C.c_uint64]
+        l.or_trainer_set_env_streams(self.h, stride)
+
+    def env_streams(self):
+        l = lib()
+        l.or_trainer_env_streams.restype = C.POINTER(C.c_uint32)
+        l.or_trainer_env_streams.argtypes = [C.c_void_p]
+        p = l.or_trainer_env_streams(self.h)
+        return np.array([p[i] for i in range(self.N)], np.uint32)
+
     def rollout(self, forced=None):
         if forced is not None:
             forced = np.ascontiguousarray(forced, np.int32)

@@ -114,6 +114,10 @@ FIXTURES = {
     # BASELINE config 1 (REINFORCE, 1-D, 8 bins, 1 env, full MLP[32])
     "pg_b8d1": ("learn", ["algo=pg", "B=8", "D=1", "widths=32", "N=1",
                           "episodes=4", "iters=3", "seed=17"]),
+    # pg_training.cc's network (full 32->256->128->8, softmax-xent) with one
+    # worker playing 4 episodes per iteration (one engine stream)
+    "pg_b8d2": ("learn", ["algo=pg", "B=8", "D=2", "widths=256,128", "N=1",
+                          "episodes=4", "iters=3", "seed=19"]),
 }
 
 

@@ -104,7 +104,7 @@ def test_weights20_logits_and_argmax_episodes():
 
 # ------------------------------------------------------------- learners ----
 LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1",
-         "klppo_b8d2", "ppo_adam_b8d2", "ac_mom_b8d2"]
+         "klppo_b8d2", "ppo_adam_b8d2", "ac_mom_b8d2", "pg_b8d2"]
 ALGO = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG, "klppo": po.OR_KLPPO}
 OPT = {"sgd": po.OPT_SGD, "momentum": po.OPT_MOMENTUM, "adam": po.OPT_ADAM}
 
@@ -181,6 +181,25 @@ def run_oracle_against(name, forced=True):
 def test_learner_matches_reference(name):
     worst = run_oracle_against(name, forced=True)
     print(name, {k: "%.2e" % v for k, v in worst.items()})
+
+
+def test_env_streams_single_env_is_reference_stream():
+    """or_trainer_set_env_streams (the device REINFORCE convention: env g on
+    the stream advanced by g * 2^26) leaves env 0 on the reference's engine:
+    pg_b8d1's one-worker run is reproduced with it on."""
+    g = golden("pg_b8d1")
+    kv = parse_meta(g)
+    pol, _ = models_for(kv)
+    tr = po.Trainer(po.OR_PG, 8, 1, 1, 1, pol, g["init_policy"],
+                    x0=int(g["x0"][0]), episodes=int(kv["episodes"]))
+    tr.set_env_streams(1 << 26)
+    for it in range(int(kv["iters"])):
+        tr.rollout()
+        np.testing.assert_array_equal(tr.buf(po.BUF_STEP_CHOICE),
+                                      g["it%d_step_choice" % it])
+        tr.learn()
+        assert int(tr.env_streams()[0]) == int(g["it%d_x_end" % it][0])
+        assert_close(tr.params(0), g["it%d_policy_params" % it])
 
 
 @pytest.mark.parametrize("name", ["ppo_adam_b8d2", "ac_mom_b8d2", "klppo_b8d2"])
