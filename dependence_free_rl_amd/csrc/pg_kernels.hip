@@ -123,6 +123,21 @@ hipError_t launch_pg_env_init(const EnvDesc &env, Batch b, uint32_t x0,
   return hipGetLastError();
 }
 
+// xh_trainer_seed_streams for REINFORCE: env g <- x advanced by g * stride.
+__global__ void pg_seed_kernel(Batch b, uint32_t x, int env_offset,
+                               uint64_t stride) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < b.N;
+       e += gridDim.x * blockDim.x)
+    b.rng[e] = mstd_jump(x, ((uint64_t)env_offset + e) * stride);
+}
+
+hipError_t launch_pg_seed(Batch b, uint32_t x, int env_offset, uint64_t stride,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(pg_seed_kernel, dim3((b.N + 255) / 256), dim3(256), 0, s,
+                     b, x, env_offset, stride);
+  return hipGetLastError();
+}
+
 // Iteration start: every env active, no steps, no episodes.
 __global__ void pg_begin_kernel(int N, int *active, int *ep_done, int *len) {
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < N;

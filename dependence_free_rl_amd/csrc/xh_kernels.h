@@ -205,6 +205,8 @@ struct PgLearnArgs {
 };
 hipError_t launch_pg_env_init(const EnvDesc &env, Batch b, uint32_t x0,
                               int env_offset, uint64_t stride, hipStream_t s);
+hipError_t launch_pg_seed(Batch b, uint32_t x, int env_offset, uint64_t stride,
+                          hipStream_t s);
 hipError_t launch_pg_begin(int N, int *active, int *ep_done, int *len,
                            hipStream_t s);
 hipError_t launch_pg_step(const PgStepArgs &a, hipStream_t s);

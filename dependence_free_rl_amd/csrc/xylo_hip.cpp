@@ -1298,6 +1298,11 @@ int xh_trainer_seed_streams(xh_trainer *t, uint32_t x) {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
     x %= 2147483647u;
     HIPCHK(hipSetDevice(t->ctx->device));
+    if (t->cfg.algo == XH_PG) {
+      HIPCHK(xh::launch_pg_seed(t->batch(), x ? x : 1u, t->cfg.env_offset,
+                                kEvalStride, t->ctx->stream));
+      return XH_OK;
+    }
     HIPCHK(xh::launch_env_seed(t->batch(), x ? x : 1u, t->cfg.env_offset,
                                t->ctx->stream));
     return XH_OK;

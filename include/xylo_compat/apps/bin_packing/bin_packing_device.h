@@ -85,6 +85,33 @@ inline policy_shape parse_policy(const xylo::model &m) {
   if (ls.size() == 6) s.head = int(ls[5]->kind());
   return s;
 }
+// REINFORCE's policy (pg_training.cc:10-20): full(4B,h1)-relu
+// [-full(h1,h2)-relu]-full(.,B)-softmax_cross_entropy.
+inline policy_shape parse_full_policy(const xylo::model &m) {
+  using K = xylo::layer_kind;
+  auto ls = m.layers();
+  auto is = [&](std::size_t i, K k) { return i < ls.size() && ls[i]->kind() == k; };
+  policy_shape s;
+  const std::size_t n = ls.size();
+  bool ok = (n == 4 || n == 6) && is(0, K::full) && is(1, K::relu) &&
+            is(n - 2, K::full) && is(n - 1, K::softmax_xent) &&
+            ls[0]->input_size() == observation::length() &&
+            ls[n - 2]->output_size() == num_bins;
+  if (ok && n == 6)
+    ok = is(2, K::full) && is(3, K::relu) &&
+         ls[2]->input_size() == ls[0]->output_size() &&
+         ls[4]->input_size() == ls[2]->output_size();
+  if (ok && n == 4) ok = ls[2]->input_size() == ls[0]->output_size();
+  if (!ok)
+    throw xeno::error("xylo-hip: the device REINFORCE policy is full(4*num_bins,"
+                      "h1)-relu[-full(h1,h2)-relu]-full(.,num_bins)-"
+                      "softmax_cross_entropy_layer");
+  s.h1 = int(ls[0]->output_size());
+  s.h2 = n == 6 ? int(ls[2]->output_size()) : 0;
+  s.head = int(K::softmax_xent);
+  return s;
+}
+
 inline std::pair<int, int> parse_value(const xylo::model &m) {
   using K = xylo::layer_kind;
   auto ls = m.layers();
@@ -177,6 +204,46 @@ class session {
       evals_.push_back({&a, &env, &m, k});
   }
 
+  // agent.play_one_episode() with a stochastic device policy and a REINFORCE
+  // learner: the window is every agent's whole episodes, played on the
+  // device at the next flush (pg_training.cc:52-62).
+  void request_train_episodes(environment &env, xylo::model &m, int k) {
+    if (learned_unforgotten_)
+      throw xeno::error("xylo-hip: call replay_buffer.forget() after "
+                        "learner.step() before playing again (device windows "
+                        "do not accumulate)");
+    if (state_ == rolled)
+      throw xeno::error("xylo-hip: play_one_episode() again before "
+                        "learner.step()");
+    if (!has_learner_ || learner_.action_model != &m ||
+        learner_.kind != xylo::learner_kind::reinforce)
+      throw xeno::error("xylo-hip: training episodes need the replay buffer's "
+                        "policy_gradient_learner (REINFORCE) constructed with "
+                        "the policy's model before playing");
+    if (env.bound_session() && env.bound_session() != this)
+      throw xeno::error("xylo-hip: env is bound to another replay buffer");
+    flush_evals();
+    if (state_ == idle) {
+      window_.clear();
+      episodes_.clear();
+      state_ = pending;
+    }
+    if (!window_.empty() && window_.back() == &env) {
+      episodes_.back() += k;
+      return;
+    }
+    if (tr_) {
+      if (window_.size() >= envs_.size() || envs_[window_.size()] != &env)
+        throw xeno::error("xylo-hip: the set / order of agents changed "
+                          "between windows");
+    } else if (!first_window_.insert(&env).second) {
+      throw xeno::error("xylo-hip: an env played in two separate runs of one "
+                        "window");
+    }
+    window_.push_back(&env);
+    episodes_.push_back(k);
+  }
+
   // Runs deferred device work in request order.
   void flush() {
     roll();
@@ -185,9 +252,6 @@ class session {
 
   void learn(rb_t &, const xylo::learner_desc &d) {
     attach(d);
-    if (d.kind == xylo::learner_kind::reinforce)
-      throw xeno::error("xylo-hip: policy_gradient_learner (REINFORCE) has no "
-                        "device path in this build");
     flush_all();
     if (state_ != rolled)
       throw xeno::error("xylo-hip: learner.step() without new experience");
@@ -196,12 +260,12 @@ class session {
     state_ = idle;
     learned_unforgotten_ = true;
     learner_.action_model->mark_device_newer(this);
-    learner_.value_model->mark_device_newer(this);
+    if (learner_.value_model) learner_.value_model->mark_device_newer(this);
     ++steps_;
     if (const char *p = std::getenv("XYLO_HIP_DUMP")) {
       const std::string k = "." + std::to_string(steps_) + ".bin";
       write_params(std::string(p) + ".policy" + k, XH_POLICY);
-      write_params(std::string(p) + ".value" + k, XH_VALUE);
+      if (!pg()) write_params(std::string(p) + ".value" + k, XH_VALUE);
     }
     maybe_exit();
   }
@@ -216,6 +280,10 @@ class session {
     flush_all();
     if (!tr_ || materialised_ || (state_ != rolled && !learned_unforgotten_))
       return;
+    if (pg()) {
+      materialise_episodes(rb);
+      return;
+    }
     const int N = int(envs_.size()), T = T_, B = int(num_bins);
     std::vector<std::int8_t> bins(std::size_t(T + 1) * N * B * 2),
         items(std::size_t(T + 1) * N * 4);
@@ -257,6 +325,53 @@ class session {
     materialised_ = true;
   }
 
+  // REINFORCE window: each env's whole episodes (all frozen), env by env.
+  void materialise_episodes(rb_t &rb) {
+    const int N = int(envs_.size()), T = T_, B = int(num_bins);
+    std::vector<std::int8_t> bins(std::size_t(T + 1) * N * B * 2),
+        items(std::size_t(T + 1) * N * 4);
+    std::vector<std::int32_t> act(std::size_t(T) * N), len(N);
+    std::vector<std::uint8_t> done(std::size_t(T) * N);
+    get(XH_BUF_BINS, bins);
+    get(XH_BUF_ITEMS, items);
+    get(XH_BUF_ACTION, act);
+    get(XH_BUF_DONE, done);
+    get(XH_BUF_LEN, len);
+    auto &list = rb.trajectories();
+    list.clear();
+    for (int e = 0; e < N; ++e) {
+      xylo::trajectory<action, observation> *traj = nullptr;
+      for (int t = 0; t < len[e]; ++t) {
+        if (!traj) traj = &rb.emplace_trajectory(state_at(bins, items, t, e));
+        action a;
+        a.choice = std::size_t(act[std::size_t(t) * N + e]);
+        const bool over = done[std::size_t(t) * N + e] != 0;
+        observation end = state_at(bins, items, over ? t : t + 1, e);
+        if (over) {
+          end.bins[a.choice].first -= end.item.first;
+          end.bins[a.choice].second -= end.item.second;
+        }
+        traj->add_transition(std::move(a), over ? 0.0f : 1.0f, std::move(end));
+        if (over) {
+          traj->freeze();
+          traj = nullptr;
+        }
+      }
+    }
+    materialised_ = true;
+  }
+
+  observation state_at(const std::vector<std::int8_t> &bins,
+                       const std::vector<std::int8_t> &items, int t, int e) {
+    const int N = int(envs_.size()), B = int(num_bins);
+    observation o;
+    const std::int8_t *b = &bins[(std::size_t(t) * N + e) * B * 2];
+    for (int i = 0; i < B; ++i) o.bins[i] = {b[2 * i], b[2 * i + 1]};
+    const std::int8_t *it = &items[(std::size_t(t) * N + e) * 4];
+    o.item = {it[0], it[1]};
+    return o;
+  }
+
   // env.view() of a device-bound env: its current state on the device.
   observation device_view(int index) {
     flush_all();
@@ -265,8 +380,14 @@ class session {
         items(std::size_t(T_ + 1) * N * 4);
     get(XH_BUF_BINS, bins);
     get(XH_BUF_ITEMS, items);
+    int slot = slot_;
+    if (pg()) {  // after its last episode an env holds its post-reset state
+      std::vector<std::int32_t> len(N);
+      get(XH_BUF_LEN, len);
+      slot = len[index];
+    }
     observation o;
-    const std::size_t row = std::size_t(slot_) * N + index;
+    const std::size_t row = std::size_t(slot) * N + index;
     for (int i = 0; i < B; ++i)
       o.bins[i] = {bins[row * B * 2 + 2 * i], bins[row * B * 2 + 2 * i + 1]};
     o.item = {items[row * 4], items[row * 4 + 1]};
@@ -281,8 +402,9 @@ class session {
   void push_params() {
     if (!tr_) return;
     push(*learner_.action_model, XH_POLICY, pol_version_);
-    push(*learner_.value_model, XH_VALUE, val_version_);
+    if (learner_.value_model) push(*learner_.value_model, XH_VALUE, val_version_);
   }
+  bool pg() const { return tr_ && tr_->cfg.algo == XH_PG; }
 
  private:
   enum { idle, pending, rolled } state_ = idle;
@@ -311,6 +433,75 @@ class session {
       check(xh_trainer_get_params(t->h, which, out.data(), out.size()),
             "xh_trainer_get_params");
     });
+  }
+
+  void ensure_trainer_pg() {
+    const int N = int(window_.size());
+    for (int k : episodes_)
+      if (k != episodes_[0])
+        throw xeno::error("xylo-hip: every agent plays the same number of "
+                          "episodes per window");
+    if (tr_) {
+      if (window_.size() != envs_.size())
+        throw xeno::error("xylo-hip: fewer agents played than in the first "
+                          "window");
+      if (episodes_[0] != tr_->cfg.steps)
+        throw xeno::error("xylo-hip: episodes per window changed");
+      return;
+    }
+    const policy_shape ps = parse_full_policy(*learner_.action_model);
+    xh_config c;
+    xh_config_default(&c, XH_PG, int(num_bins), 2, N, episodes_[0]);
+    c.policy_h1 = ps.h1;
+    c.policy_h2 = ps.h2;
+    c.lr_policy = learner_.action_optimizer->rate();
+    c.wd_policy = learner_.action_optimizer->weight_decay();
+    c.gamma = learner_.gamma;
+    tr_ = std::make_unique<trainer>(c);
+    set_optimizers();
+    T_ = int(xh_trainer_buffer_bytes(tr_->h, XH_BUF_ACTION) / (4 * std::size_t(N)));
+    upload_host_states();
+    if (const char *p = std::getenv("XYLO_HIP_DUMP"))
+      write_params(std::string(p) + ".policy.0.bin", XH_POLICY);
+  }
+
+  void set_optimizers() {
+    for (int which : {XH_POLICY, XH_VALUE}) {
+      xylo::optimizer *o = which == XH_POLICY ? learner_.action_optimizer
+                                              : learner_.value_optimizer;
+      if (!o || o->kind() == xylo::optimizer_kind::sgd) continue;
+      const int kind = o->kind() == xylo::optimizer_kind::adam ? XH_OPT_ADAM
+                                                               : XH_OPT_MOMENTUM;
+      check(xh_trainer_set_optimizer(tr_->h, which, kind, o->rate(), 0.0f,
+                                     o->beta1(), o->beta2()),
+            "xh_trainer_set_optimizer");
+    }
+  }
+
+  // slot 0 <- the host envs' states (drawn by their constructors); binds them
+  void upload_host_states() {
+    const int N = int(window_.size()), B = int(num_bins);
+    std::vector<std::int8_t> bins(std::size_t(T_ + 1) * N * B * 2, 0),
+        items(std::size_t(T_ + 1) * N * 4, 0);
+    for (int e = 0; e < N; ++e) {
+      const observation &o = window_[e]->host_state();
+      for (int i = 0; i < B; ++i) {
+        bins[(std::size_t(e) * B + i) * 2] = std::int8_t(o.bins[i].first);
+        bins[(std::size_t(e) * B + i) * 2 + 1] = std::int8_t(o.bins[i].second);
+      }
+      items[std::size_t(e) * 4] = std::int8_t(o.item.first);
+      items[std::size_t(e) * 4 + 1] = std::int8_t(o.item.second);
+      window_[e]->bind(this, e);
+    }
+    check(xh_trainer_set_buffer(tr_->h, XH_BUF_BINS, bins.data(), bins.size()),
+          "xh_trainer_set_buffer");
+    check(xh_trainer_set_buffer(tr_->h, XH_BUF_ITEMS, items.data(),
+                                items.size()),
+          "xh_trainer_set_buffer");
+    envs_ = window_;
+    first_window_.clear();
+    pol_version_ = val_version_ = ~0ull;
+    push_params();
   }
 
   void ensure_trainer() {
@@ -350,16 +541,7 @@ class session {
     tr_ = std::make_unique<trainer>(c);
     // momentum / adam optimizers (nn.h:630-698) run on the device too; their
     // state starts at zero with the first learn(), as the reference's does
-    for (int which : {XH_POLICY, XH_VALUE}) {
-      xylo::optimizer *o = which == XH_POLICY ? learner_.action_optimizer
-                                              : learner_.value_optimizer;
-      if (o->kind() == xylo::optimizer_kind::sgd) continue;
-      const int kind = o->kind() == xylo::optimizer_kind::adam ? XH_OPT_ADAM
-                                                               : XH_OPT_MOMENTUM;
-      check(xh_trainer_set_optimizer(tr_->h, which, kind, o->rate(), 0.0f,
-                                     o->beta1(), o->beta2()),
-            "xh_trainer_set_optimizer");
-    }
+    set_optimizers();
     // initial env states: slot 0 from the host envs (drawn by their ctors)
     const int B = int(num_bins);
     std::vector<std::int8_t> bins(std::size_t(T_ + 1) * N * B * 2, 0),
@@ -391,6 +573,10 @@ class session {
 
   void roll() {
     if (state_ != pending) return;
+    if (!episodes_.empty()) {
+      roll_episodes();
+      return;
+    }
     ensure_trainer();
     push_params();
     auto &eng = xylo::detail::raw_generator();
@@ -402,6 +588,25 @@ class session {
     state_ = rolled;
     materialised_ = false;
     slot_ = T_;
+  }
+
+  // REINFORCE window: env g plays on the engine state advanced by g * 2^26
+  // draws (env 0 continues the host engine exactly, as one reference worker
+  // does); the host engine then takes the last env's final stream state.
+  void roll_episodes() {
+    ensure_trainer_pg();
+    push_params();
+    auto &eng = xylo::detail::raw_generator();
+    const std::uint32_t x = engine_state(eng);
+    if (steps_ == 0) x_first_ = x;
+    check(xh_trainer_seed_streams(tr_->h, x), "xh_trainer_seed_streams");
+    check(xh_trainer_rollout(tr_->h), "xh_trainer_rollout");
+    std::vector<std::uint32_t> rng(envs_.size());
+    get(XH_BUF_RNG, rng);
+    eng.seed(rng.back());
+    state_ = rolled;
+    materialised_ = false;
+    episodes_.clear();
   }
 
   void flush_evals() {
@@ -510,8 +715,10 @@ class session {
       j << "{\"x0\": " << x_first_ << ", \"num_envs\": " << envs_.size()
         << ", \"steps\": " << T_ << ", \"learner_steps\": " << steps_
         << ", \"algo\": \""
-        << (tr_->cfg.algo == XH_AC ? "ac"
-                                   : tr_->cfg.algo == XH_KLPPO ? "klppo" : "ppo")
+        << (tr_->cfg.algo == XH_AC      ? "ac"
+            : tr_->cfg.algo == XH_KLPPO ? "klppo"
+            : tr_->cfg.algo == XH_PG    ? "pg"
+                                        : "ppo")
         << "\", \"h1\": " << tr_->cfg.policy_h1 << ", \"h2\": "
         << tr_->cfg.policy_h2 << ", \"v1\": " << tr_->cfg.value_h1
         << ", \"v2\": " << tr_->cfg.value_h2 << ", \"lr_policy\": "
@@ -528,6 +735,7 @@ class session {
   std::vector<environment *> window_, envs_;
   std::set<environment *> first_window_;
   std::vector<eval_req> evals_;
+  std::vector<int> episodes_;  // REINFORCE window: episodes per env
   int T_ = 0, slot_ = 0;
   bool materialised_ = false, learned_unforgotten_ = false;
   long steps_ = 0;
@@ -594,10 +802,17 @@ template <> struct device_traits<bp::action, bp::observation> {
     return true;
   }
   static bool play_episodes(agent<A, S> &a, int k) {
+    auto *env = dynamic_cast<bp::environment *>(&a.bound_env());
+    if (!env) return false;
+    if (auto *sp = dynamic_cast<const policy_gradient_policy<A, S> *>(
+            &a.bound_policy())) {  // REINFORCE training episodes
+      bp::device::session_of(a.bound_buffer())
+          .request_train_episodes(*env, sp->device_model(), k);
+      return true;
+    }
     auto *p = dynamic_cast<const policy_gradient_deterministic_policy<A, S> *>(
         &a.bound_policy());
-    auto *env = dynamic_cast<bp::environment *>(&a.bound_env());
-    if (!p || !env) return false;
+    if (!p) return false;
     bp::device::session_of(a.bound_buffer())
         .request_episodes(a, *env, p->device_model(), k);
     return true;

@@ -210,7 +210,9 @@ int xh_heuristic_evaluate(xh_ctx *ctx, int policy, int bins, int dims,
  * next rollout steps env g (global index) from x advanced by 4*T*g draws, i.e.
  * the reference order in which worker 0 plays its T steps, then worker 1, ...
  * (ppo_training.cc:53-62 run sequentially, 4 draws per step).  After that
- * rollout the global engine is at x advanced by 4*T*num_envs_global. */
+ * rollout the global engine is at x advanced by 4*T*num_envs_global.
+ * XH_PG: env g's stream <- x advanced by g * 2^26 draws (env 0 continues the
+ * engine as a single reference worker does). */
 int xh_trainer_seed_streams(xh_trainer *t, uint32_t x);
 
 /* sizeof of the ABI structs ("xh_config", "xh_eval"; 0 if unknown), so a

@@ -585,11 +585,16 @@ uint32_t or_trainer_rng(const or_trainer *t) { return t->x; }
 /* Independent per-env streams: env i draws from x0 advanced by i * stride
  * (the device evaluators' and REINFORCE trainer's convention; env 0 is the
  * single-env reference run).  Re-constructs the envs (2 draws each). */
-void or_trainer_set_env_streams(or_trainer *t, uint64_t stride) {
+void or_trainer_set_env_streams(or_trainer *t, uint64_t stride,
+                                int reconstruct) {
   const int BD = t->env.B * t->env.D;
   free(t->xs);
   t->xs = (uint32_t *)malloc(sizeof(uint32_t) * t->N);
   for (int i = 0; i < t->N; ++i) {
+    if (!reconstruct) { /* keep the envs; streams from the current engine */
+      t->xs[i] = or_minstd_jump(t->x, (uint64_t)i * stride);
+      continue;
+    }
     t->xs[i] = or_minstd_jump(t->x0, (uint64_t)i * stride);
     or_env_construct(&t->env, t->bins + (size_t)i * BD,
                      t->item + (size_t)i * 3, &t->xs[i]);

@@ -110,8 +110,12 @@ void or_trainer_rollout(or_trainer *t, const int32_t *forced);
 void or_trainer_learn(or_trainer *t); /* learn() + replay_buffer.forget() */
 uint32_t or_trainer_rng(const or_trainer *t);
 /* Per-env streams: env i draws from x0 advanced by i * stride (env 0 = the
- * single-env reference run); re-constructs the envs on those streams. */
-void or_trainer_set_env_streams(or_trainer *t, uint64_t stride);
+ * single-env reference run), re-constructing the envs on those streams; or,
+ * with reconstruct = 0, keeps the envs (constructed in worker order on the
+ * shared engine) and starts env i's stream at the engine state advanced by
+ * i * stride (the drop-in layer's REINFORCE windows). */
+void or_trainer_set_env_streams(or_trainer *t, uint64_t stride,
+                                int reconstruct);
 const uint32_t *or_trainer_env_streams(const or_trainer *t);
 void or_trainer_get_params(const or_trainer *t, int which, float *out);
 void or_trainer_set_params(or_trainer *t, int which, const float *in);

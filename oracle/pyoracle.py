@@ -237,11 +237,13 @@ class Trainer:
                                                C.c_float]
         l.or_trainer_set_optimizer(self.h, which, kind, lr, wd, beta1, beta2)
 
-    def set_env_streams(self, stride=1 << 26):
-        """Env i on its own stream: x0 advanced by i * stride."""
+    def set_env_streams(self, stride=1 << 26, reconstruct=True):
+        """Env i on its own stream: x0 advanced by i * stride (reconstructing
+        the envs), or the current engine advanced by i * stride (keeping
+        them)."""
         l = lib()
-        l.or_trainer_set_env_streams.argtypes = [C.c_void_p, C.c_uint64]
-        l.or_trainer_set_env_streams(self.h, stride)
+        l.or_trainer_set_env_streams.argtypes = [C.c_void_p, C.c_uint64, C.c_int]
+        l.or_trainer_set_env_streams(self.h, stride, 1 if reconstruct else 0)
 
     def env_streams(self):
         l = lib()

@@ -77,6 +77,42 @@ def test_reference_driver_on_gpu(tmp_path, name):
     assert np.isfinite(np.fromfile(prefix + ".policy.2.bin", np.float32)).all()
 
 
+def test_pg_training_on_gpu(tmp_path):
+    """pg_training.cc unmodified: 4 workers x 4 episodes per window on the
+    device (bp::pg_learner = REINFORCE).  Worker g plays on the engine state
+    advanced by g * 2^26 draws (worker 0 continues the engine as the
+    reference's own single-threaded order does).  The logged average and the
+    parameters after learner.step() match the oracle run the same way."""
+    import re
+    import subprocess
+    from oracle import pyoracle as po
+    _need("pg_training")
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, XYLO_SEED="7", XYLO_HIP_MAX_STEPS="2",
+               XYLO_HIP_DUMP=prefix)
+    r = subprocess.run([app("pg_training")], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = re.search(r"avg rewards 0 :([-+0-9.eE]+)", r.stderr + r.stdout)
+    assert m, r.stderr[-2000:]
+    meta = json.load(open(prefix + ".json"))
+    assert meta["algo"] == "pg" and meta["num_envs"] == 4
+    pol0 = np.fromfile(prefix + ".policy.0.bin", np.float32)
+    x_first = int(meta["x0"])
+    # the 4 envs were constructed (2 draws each) right before the first window
+    x_models = po.minstd_jump(x_first, 2147483646 - 8)
+    pm = po.full_model(32, [256, 128], 8, po.OR_SOFTMAX_XENT)
+    orc = po.Trainer(po.OR_PG, 8, 2, 4, 1, pm, pol0, x0=x_models, episodes=4)
+    orc.set_env_streams(1 << 26, reconstruct=False)
+    orc.rollout()
+    steps = len(orc.buf(po.BUF_STEP_CHOICE))
+    assert float(m.group(1)) == fmt6(steps / 16.0)
+    orc.learn()
+    pol1 = np.fromfile(prefix + ".policy.1.bin", np.float32)
+    assert_close(pol1, orc.params(0), what="pg_training policy after step 1")
+    assert np.isfinite(np.fromfile(prefix + ".policy.2.bin", np.float32)).all()
+
+
 def test_deep_agent_first_round(tmp_path):
     _need("deep_agent")
     g = golden("deep_w20")
