@@ -22,8 +22,6 @@
 #include "xh_device.h"
 #include "xh_kernels.h"
 
-#include <cstdlib>
-
 namespace xh {
 
 template <int B_, int D_, int H1_, int H2_>
@@ -65,13 +63,6 @@ struct PShape {
   static constexpr int L_H1T = L_ROLLOUT_END;
   static constexpr int L_DAT = L_H1T + H1 * TS;
   static constexpr int L_TRAIN8_END = L_DAT + H2 * TS;
-  // team kernel: two dL/dA2 buffers [H2][TS] + two row-feature buffers
-  // [64][FP] (+ the group's item flag)
-  static constexpr int FP = r4(F0);
-  static constexpr int XBS = 64 * FP + 4;
-  static constexpr int L_TEAM = L_ROLLOUT_END;
-  static constexpr int L_XB = L_TEAM + 2 * H2 * TS;
-  static constexpr int L_TEAM_END = L_XB + 2 * XBS;
   // end-of-kernel reduction scratch (aliases the H1 / dA2 images)
   static constexpr int RED = H1 * F0 + H1 + 2 * H2 + 1;
   static_assert(4 * RED <= 64 * HS + 64 * AS, "scratch fits");
@@ -1030,14 +1021,31 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   // Layer 1 tile by tile, fused into the layer-2 k-loop, for this wave's
   // H2 tile q of r-tile rt; optionally writes its H1 tile q to the image.
   auto forward = [&](bool write_h1) {
-    f32x16 pre = zero16();
+    // accumulators start from the biases (no separate bias pass)
+    f32x16 pre;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
+      pre[4 * qq + 0] = bb.x;
+      pre[4 * qq + 1] = bb.y;
+      pre[4 * qq + 2] = bb.z;
+      pre[4 * qq + 3] = bb.w;
+    }
     float xb[S::S1];
 #pragma unroll
     for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
     const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
-      f32x16 t1 = zero16();
+      f32x16 t1;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
+        t1[4 * qq + 0] = bb.x;
+        t1[4 * qq + 1] = bb.y;
+        t1[4 * qq + 2] = bb.z;
+        t1[4 * qq + 3] = bb.w;
+      }
 #pragma unroll
       for (int s = 0; s < S::S1; ++s) {
         const int k = 2 * s + h;
@@ -1045,15 +1053,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         t1 = mfma32(wa, xb[s], t1);
       }
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
-        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float v = t1[4 * qq + u] + bq[u];
-          t1[4 * qq + u] = v > 0.0f ? v : 0.0f;
-        }
-      }
+      for (int j = 0; j < 16; ++j) t1[j] = t1[j] > 0.0f ? t1[j] : 0.0f;
       if (write_h1 && it == q) {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
@@ -1068,14 +1068,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         pre = mfma32(a4.z, t1[4 * qq + 2], pre);
         pre = mfma32(a4.w, t1[4 * qq + 3], pre);
       }
-    }
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
-      pre[4 * qq + 0] += bb.x;
-      pre[4 * qq + 1] += bb.y;
-      pre[4 * qq + 2] += bb.z;
-      pre[4 * qq + 3] += bb.w;
     }
     return pre;
   };
@@ -1215,7 +1207,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       };
       // SIMD partners (waves w and w + 4) run this interval in opposite
       // orders, so one's dW1 VALU tail sits beside the other's MFMAs.
-      const bool swap = (a.ablate & 32) && rt == 1;
+      const bool swap = !(a.ablate & 32) && rt == 1;  // bit 5: same order
       if (!swap) dw2();
 
       // ---- dH1 tile q of r-tile rt (K = H2); relu'; dW1, db1
@@ -1233,13 +1225,15 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         bool item_is_a = true;
 #pragma unroll
         for (int d = 0; d < S::D; ++d) item_is_a &= iv_c[d] == a.env.item_a[d];
+        // d * 1 and d * 0 are exact: sA / sB take d or nothing
+        const float fa = item_is_a ? 1.0f : 0.0f, fb = 1.0f - fa;
         const float *hcol = H1T + (q * 32) * S::TS + rt * 32 + lr;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           // relu' from the H1 image (post-relu > 0 <=> pre > 0)
           const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
-          sA[j] += item_is_a ? d : 0.0f;
-          sB[j] += item_is_a ? 0.0f : d;
+          sA[j] = fmaf(d, fa, sA[j]);
+          sB[j] = fmaf(d, fb, sB[j]);
 #pragma unroll
           for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
         }
@@ -1327,360 +1321,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   }
 }
 
-// ============================ train epoch, forward / backward wave teams ====
-// B = 64, H1 = H2 = 128 (BASELINE config 3 policy): a group is one env step
-// (64 rows).  Waves 0-3 (forward team) and 4-7 (backward team) pair up on
-// the four SIMDs and work one group apart: in interval k the forward team
-// runs group k's forward pass, softmax and loss gradient and writes dL/dA2
-// into LDS buffer k&1, while the backward team runs group k-1's weight and
-// data gradients from buffer (k-1)&1.  A SIMD's two waves are thus always in
-// different phases, so one's VALU / LDS / barrier time issues beside the
-// other's MFMAs (in policy_train8_kernel the partners stall together).
-//   forward wave q:  H2 tile q of both r-tiles (layer 1 fused tile by tile
-//                    into the layer-2 k-loop); dw3, db2 of tile q
-//   backward wave q: dW2 tiles (q, 0..3), K = the group's 64 rows, with H1
-//                    recomputed transposed (rows in accumulator registers) as
-//                    the B operand; dH1 tile q of both r-tiles; dW1, db1
-// Two H1 images would not fit beside the double buffer, hence the recompute
-// (+20 K=2 MFMAs per wave and group, ~5% more MFMA work).  Every gradient
-// entry has exactly one owning wave, so the slab is written straight from
-// registers after a 32-lane reduction (deterministic).
-template <class S>
-__global__ __launch_bounds__(512, 2) void policy_train_team_kernel(PolicyTrainArgs a) {
-  static_assert(S::NIT == 4 && S::NOT == 4 && S::B == 64 && S::HG == 1,
-                "team kernel: B = 64, H1 = H2 = 128");
-  static_assert(sizeof(float) * S::L_TEAM_END <= 160 * 1024, "LDS");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  stage_params<S>(a.params, lds);
-  __syncthreads();
-  constexpr int D = S::D, F0 = S::F0, S1 = S::S1, FP = S::FP, TS = S::TS;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
-            h = lane >> 5;
-  const int q = w & 3;
-  const bool fwd = w < 4;
-  const int ngroups = a.b.T * a.b.N;  // group g = env step t*N + e
-  const int n = (int)blockIdx.x < ngroups
-                    ? (ngroups - 1 - (int)blockIdx.x) / (int)gridDim.x + 1
-                    : 0;
-
-  // Loop-carried accumulators.  accP / accQ hold dw3 / db2 of H2 tile q in
-  // the forward team, and sA / sB (the dA1 sums over rows holding item_a /
-  // item_b, bin_packing.h:73-74) of H1 tile q in the backward team.
-  f32x16 accW2[4];
-  float accW1[16][D], accP[16], accQ[16], accB3 = 0.0f;
-#pragma unroll
-  for (int it = 0; it < 4; ++it) accW2[it] = zero16();
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    accP[j] = accQ[j] = 0.0f;
-#pragma unroll
-    for (int f = 0; f < D; ++f) accW1[j][f] = 0.0f;
-  }
-
-  // forward team: raw int8 state of rows rt*32 + lr, fetched a group ahead
-  int bv_c[2][D], iv_c[D], bv_n[2][D], iv_n[D];
-  auto fetch = [&](int k, int (&bv)[2][D], int (&iv)[D]) {
-    const size_t g = (size_t)blockIdx.x + (size_t)k * gridDim.x;
-    const int8_t *bp = a.b.bins + g * S::BD;
-    const int8_t *ip = a.b.items + g * 4;
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int d = 0; d < D; ++d) bv[rt][d] = bp[(rt * 32 + lr) * D + d];
-#pragma unroll
-    for (int d = 0; d < D; ++d) iv[d] = ip[d];
-  };
-  if (fwd && n > 0) fetch(0, bv_c, iv_c);
-
-  f32x16 pre[2];
-  int c_cur = 0;
-  float po_cur = 1.0f, A_cur = 0.0f;
-  for (int k = 0; k <= n; ++k) {
-    // ------------------------------------------------------ interval part 1
-    if (fwd) {
-      if (k < n) {
-        const int g = blockIdx.x + k * gridDim.x;
-        if (k + 1 < n) fetch(k + 1, bv_n, iv_n);
-        c_cur = a.b.action[g];
-        po_cur = a.b.pold[g];
-        A_cur = a.adv[g];
-        // observation features (bin dims / 8, item dims / 8) of this lane's
-        // rows; wave 0 hands them (and the item type) to the backward team
-        float *xbw = lds + S::L_XB + (k & 1) * S::XBS;
-        float xb[2][S1];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-          for (int s = 0; s < S1; ++s) {
-            const int f = 2 * s + h;
-            int v = 0;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-              if (f == d) v = bv_c[rt][d];
-              if (f == D + d) v = iv_c[d];
-            }
-            xb[rt][s] = (float)v / (float)kCapacity;
-            if (q == 0) xbw[(rt * 32 + lr) * FP + f] = xb[rt][s];
-          }
-        if (q == 0 && lane == 0) {
-          bool is_a = true;
-#pragma unroll
-          for (int d = 0; d < D; ++d) is_a &= iv_c[d] == a.env.item_a[d];
-          xbw[64 * FP] = is_a ? 1.0f : 0.0f;
-        }
-        // layer 1 (bias-initialised accumulators) fused into layer 2
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float4 bb = lds4(lds + S::L_B2 + q * 32 + 8 * qq + 4 * h);
-          pre[0][4 * qq + 0] = pre[1][4 * qq + 0] = bb.x;
-          pre[0][4 * qq + 1] = pre[1][4 * qq + 1] = bb.y;
-          pre[0][4 * qq + 2] = pre[1][4 * qq + 2] = bb.z;
-          pre[0][4 * qq + 3] = pre[1][4 * qq + 3] = bb.w;
-        }
-        const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          f32x16 t1[2];
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
-            t1[0][4 * qq + 0] = t1[1][4 * qq + 0] = bb.x;
-            t1[0][4 * qq + 1] = t1[1][4 * qq + 1] = bb.y;
-            t1[0][4 * qq + 2] = t1[1][4 * qq + 2] = bb.z;
-            t1[0][4 * qq + 3] = t1[1][4 * qq + 3] = bb.w;
-          }
-#pragma unroll
-          for (int s = 0; s < S1; ++s) {
-            const float wa = lds[S::L_W1 + (it * 32 + lr) * F0 + 2 * s + h];
-            t1[0] = mfma32(wa, xb[0][s], t1[0]);
-            t1[1] = mfma32(wa, xb[1][s], t1[1]);
-          }
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            t1[0][j] = t1[0][j] > 0.0f ? t1[0][j] : 0.0f;
-            t1[1][j] = t1[1][j] > 0.0f ? t1[1][j] : 0.0f;
-          }
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
-            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              pre[0] = mfma32(av[u], t1[0][4 * qq + u], pre[0]);
-              pre[1] = mfma32(av[u], t1[1][4 * qq + u], pre[1]);
-            }
-          }
-        }
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const float zp = logit_part<S>(lds, pre[rt], q);
-          if (lane < 32) lds[S::L_Z + q * 64 + rt * 32 + lr] = zp;
-        }
-      }
-    } else if (k >= 1) {
-      // dW2 tiles (q, it) of group k-1.  ht = H1 of r-tile rt transposed:
-      // acc register m of lane (i, h) = row rt*32 + acc_row(m, h) of unit
-      // it*32 + i, so MFMA step m pairs it with dA2 of the same row, 4 steps
-      // per ds_read_b128 of the dA2 image.
-      const float *xbr = lds + S::L_XB + ((k - 1) & 1) * S::XBS;
-      const float *da = lds + S::L_TEAM + ((k - 1) & 1) * S::H2 * TS +
-                        (q * 32 + lr) * TS + 4 * h;
-      float xb[2][S1];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int s = 0; s < S1; ++s) xb[rt][s] = xbr[(rt * 32 + lr) * FP + 2 * s + h];
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        float wa[S1];
-#pragma unroll
-        for (int s = 0; s < S1; ++s)
-          wa[s] = lds[S::L_W1 + (it * 32 + lr) * F0 + 2 * s + h];
-        const float bias = lds[S::L_B1 + it * 32 + lr];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          f32x16 ht;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) ht[j] = bias;
-#pragma unroll
-          for (int s = 0; s < S1; ++s) ht = mfma32(xb[rt][s], wa[s], ht);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) ht[j] = ht[j] > 0.0f ? ht[j] : 0.0f;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float4 av = lds4(da + rt * 32 + 8 * u);
-            accW2[it] = mfma32(av.x, ht[4 * u + 0], accW2[it]);
-            accW2[it] = mfma32(av.y, ht[4 * u + 1], accW2[it]);
-            accW2[it] = mfma32(av.z, ht[4 * u + 2], accW2[it]);
-            accW2[it] = mfma32(av.w, ht[4 * u + 3], accW2[it]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-
-    // ------------------------------------------------------ interval part 2
-    if (fwd) {
-      if (k < n) {
-        // logits -> softmax -> loss gradient w.r.t. logits (lane = row = bin)
-        float gz;
-        {
-          const float zs = ((lds[S::L_Z + lane] + lds[S::L_Z + 64 + lane]) +
-                            lds[S::L_Z + 128 + lane]) + lds[S::L_Z + 192 + lane];
-          const float z = zs + lds[S::L_B3];
-          const float ex = expf(z);
-          const float p = ex / seg_sum<64>(ex);
-          const int c = c_cur;
-          const float A = A_cur;
-          if (a.algo == kPPO) {
-            // clipped_gradient (rl.h:54-74) + softmax_layer::backward
-            // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
-            const float pc = wave_shfl(p, c);
-            const float ratio = pc / po_cur;
-            float clipped = ratio;
-            if (ratio > 1.0f + a.clip_eps)
-              clipped = 1.0f + a.clip_eps;
-            else if (ratio < 1.0f - a.clip_eps)
-              clipped = 1.0f - a.clip_eps;
-            const float ig = fminf(clipped * A, ratio * A) * -1.0f;
-            const float gc = ig / pc;
-            const float lin = lane == c ? p : 0.0f;
-            gz = (lin - p * pc) * gc;
-          } else {
-            // softmax_gradient_log (rl.h:45-52) through softmax-xent
-            gz = p * A;
-            if (lane == c) gz -= A;
-          }
-          accB3 += gz;
-        }
-        // layer 3 and the layer-2 relu backward -> dA2 image (k & 1)
-        float *dab = lds + S::L_TEAM + (k & 1) * S::H2 * TS;
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const float gr = wave_shfl(gz, rt * 32 + lr);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
-            const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int j = 4 * qq + u;
-              const float v = pre[rt][j];
-              accP[j] += gr * (v > 0.0f ? v : 0.0f);
-              const float d = v > 0.0f ? gr * wq[u] : 0.0f;
-              accQ[j] += d;
-              dab[(q * 32 + acc_row(j, h)) * TS + rt * 32 + lr] = d;
-            }
-          }
-        }
-      }
-    } else if (k >= 1) {
-      // dH1 tile q of both r-tiles (K = H2), relu' from layer-1 tile q
-      // recomputed exactly as the forward team computed it; dW1, db1
-      const float *dak = lds + S::L_TEAM + ((k - 1) & 1) * S::H2 * TS;
-      const float *xbr = lds + S::L_XB + ((k - 1) & 1) * S::XBS;
-      f32x16 dh[2];
-      dh[0] = zero16();
-      dh[1] = zero16();
-#pragma unroll 8
-      for (int s = 0; s < S::H2 / 2; ++s) {
-        const int kk = 2 * s + h;
-        const float av = lds[S::L_W2 + kk * S::W2S + q * 32 + lr];
-        dh[0] = mfma32(av, dak[kk * TS + lr], dh[0]);
-        dh[1] = mfma32(av, dak[kk * TS + 32 + lr], dh[1]);
-      }
-      const float fa = xbr[64 * FP], fb = 1.0f - fa;  // item_a: 1, item_b: 0
-      float wa[S1];
-#pragma unroll
-      for (int s = 0; s < S1; ++s)
-        wa[s] = lds[S::L_W1 + (q * 32 + lr) * F0 + 2 * s + h];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        f32x16 t1;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float4 bb = lds4(lds + S::L_B1 + q * 32 + 8 * qq + 4 * h);
-          t1[4 * qq + 0] = bb.x;
-          t1[4 * qq + 1] = bb.y;
-          t1[4 * qq + 2] = bb.z;
-          t1[4 * qq + 3] = bb.w;
-        }
-        const float *xrow = xbr + (rt * 32 + lr) * FP;
-#pragma unroll
-        for (int s = 0; s < S1; ++s) t1 = mfma32(wa[s], xrow[2 * s + h], t1);
-        float xr[D];  // bin features of this lane's row
-#pragma unroll
-        for (int f = 0; f < D; ++f) xr[f] = xrow[f];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float d = t1[j] > 0.0f ? dh[rt][j] : 0.0f;
-          // d * 1 and d * 0 are exact: sA / sB get d or nothing
-          accP[j] = fmaf(d, fa, accP[j]);
-          accQ[j] = fmaf(d, fb, accQ[j]);
-#pragma unroll
-          for (int f = 0; f < D; ++f) accW1[j][f] += d * xr[f];
-        }
-      }
-    }
-    __syncthreads();
-    if (fwd) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        bv_c[0][d] = bv_n[0][d];
-        bv_c[1][d] = bv_n[1][d];
-        iv_c[d] = iv_n[d];
-      }
-    }
-  }
-
-  // ---------------------------------------------------- slab write-out ----
-  const PolicyLayout L{F0, S::H1, S::H2};
-  float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
-  if (!fwd) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        slab[L.oW2() + (q * 32 + acc_row(j, h)) * S::H1 + it * 32 + lr] =
-            accW2[it][j];
-  }
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    float vp = accP[j], vq = accQ[j], vw1[D];
-#pragma unroll
-    for (int f = 0; f < D; ++f) vw1[f] = accW1[j][f];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      vp += __shfl_xor(vp, o, kWave);
-      vq += __shfl_xor(vq, o, kWave);
-#pragma unroll
-      for (int f = 0; f < D; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
-    }
-    if (lr == 0) {
-      const int i = q * 32 + acc_row(j, h);
-      if (fwd) {
-        slab[L.ow3() + i] = vp;
-        slab[L.ob2() + i] = vq;
-      } else {
-#pragma unroll
-        for (int f = 0; f < D; ++f) slab[L.oW1() + i * F0 + f] = vw1[f];
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-          slab[L.oW1() + i * F0 + D + d] =
-              vp * ((float)a.env.item_a[d] / (float)kCapacity) +
-              vq * ((float)a.env.item_b[d] / (float)kCapacity);
-        slab[L.ob1() + i] = vp + vq;
-      }
-    }
-  }
-  if (w == 0) {
-    float v = accB3;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
-    if (lane == 0) slab[L.ob3()] = v;
-  }
-}
-
 // ================================================================ dispatch ==
 #define XH_POLICY_SHAPES(X) \
   X(8, 2, 128, 64)          \
@@ -1702,17 +1342,6 @@ template <class S>
 constexpr size_t train_lds() {
   return sizeof(float) *
          (S::L_TRAIN_END > S::L_TRAIN8_END ? S::L_TRAIN_END : S::L_TRAIN8_END);
-}
-
-template <class S>
-constexpr size_t team_lds() {
-  return sizeof(float) * S::L_TEAM_END;
-}
-// XH_TRAIN_KERNEL=8 selects policy_train8_kernel where the team kernel would
-// run (A/B measurements and the agreement test); read at every launch.
-static bool force_train8() {
-  const char *e = std::getenv("XH_TRAIN_KERNEL");
-  return e && std::atoi(e) == 8;
 }
 
 bool policy_shape_supported(int B, int D, int H1, int H2) {
@@ -1825,10 +1454,6 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
         (void)hipFuncSetAttribute((const void *)policy_train8_kernel<S>,     \
                                   hipFuncAttributeMaxDynamicSharedMemorySize,\
                                   (int)train_lds<S>());                      \
-      if constexpr (S::NIT == 4 && S::NOT == 4 && S::B == 64)                \
-        (void)hipFuncSetAttribute((const void *)policy_train_team_kernel<S>, \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,\
-                                  (int)team_lds<S>());                       \
       attr = true;                                                           \
     }                                                                        \
     if (a.algo == kKLPPO) {                                                  \
@@ -1838,13 +1463,6 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
       else                                                                   \
         return hipErrorInvalidValue;                                         \
       return hipGetLastError();                                              \
-    }                                                                        \
-    if constexpr (S::NIT == 4 && S::NOT == 4 && S::B == 64 && !XH_TRAIN4) { \
-      if (!a.ablate && !force_train8()) {                                    \
-        hipLaunchKernelGGL(policy_train_team_kernel<S>, dim3(grid),          \
-                           dim3(512), team_lds<S>(), s, a);                  \
-        return hipGetLastError();                                            \
-      }                                                                      \
     }                                                                        \
     if constexpr (S::NIT == 4 && S::NOT == 4 && (!XH_TRAIN4 || S::HG > 1))  \
       hipLaunchKernelGGL(policy_train8_kernel<S>, dim3(grid), dim3(512),     \

@@ -265,15 +265,27 @@ __global__ void transpose_kernel(const float *src, float *dst, int rows,
   }
 }
 
-// Deterministic slab reduction: out[i] = sum over slabs in slab order.
-__global__ void slab_reduce_kernel(const float *slab, int nslab, int stride,
-                                   int n, float *out) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * stride + i];
-    out[i] = s;
+// Deterministic slab reduction: out[i] = sum over slabs in a fixed order.
+// A 256-thread block takes 64 consecutive entries x 4 slab ranges (each
+// wave reads 256-byte rows, enough blocks to cover the chip); the 4 range
+// sums combine in LDS as (s0 + s1) + (s2 + s3).
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
+                                                          int nslab, int stride,
+                                                          int n, float *out) {
+  __shared__ float part[4][64];
+  const int p = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + p;
+  const int per = (nslab + 3) / 4, k0 = r * per,
+            k1 = k0 + per < nslab ? k0 + per : nslab;
+  float s = 0.0f;
+  if (i < n) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += slab[(size_t)k * stride + i];
   }
+  part[r][p] = s;
+  __syncthreads();
+  if (r == 0 && i < n)
+    out[i] = (part[0][p] + part[1][p]) + (part[2][p] + part[3][p]);
 }
 
 // sgd_optimizer::next_parameters (nn.h:622-625): p * (1 - wd) - g * lr
@@ -394,7 +406,7 @@ hipError_t launch_transpose(const float *src, float *dst, int rows, int cols,
 
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s) {
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks_for(n)), dim3(256), 0, s,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, s,
                      slab, nslab, stride, n, out);
   return hipGetLastError();
 }

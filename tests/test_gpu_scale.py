@@ -31,6 +31,7 @@ def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
 
 @pytest.mark.parametrize("algo,B,D,widths,N,T", [
     ("ppo", 64, 2, (128, 128), 32, 4),   # BASELINE config 3 shape
+    ("ppo", 64, 2, (128, 128), 160, 4),  # 640 groups: multi-group train blocks
     ("ppo", 32, 1, (64, 64), 64, 4),     # config 2 shape
     ("ac", 16, 2, (64, 64), 64, 8),
     ("ac", 128, 3, (128, 128), 8, 8),    # config 5 shape
@@ -133,3 +134,24 @@ def test_c3_full_size_properties(ctx):
     tr2 = make()
     tr2.iterate(3)
     np.testing.assert_array_equal(tr2.params(POLICY), p1)
+
+
+def test_c3_rng_positions_full_size(ctx):
+    """Every env's minstd state after 2 iterations at full config-3 size sits
+    at its reference-order position: 2 construction draws per
+    env, then 4 draws per env step in worker order, i.e.
+    jump(x0, 2N + 4TN*its + 4T*e)."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import BUF_RNG
+    N, B, D, T, its, x0 = 32768, 64, 2, 4, 2, 1234567
+    tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
+                 rng_state=x0)
+    tr.set_params(POLICY, init_policy(D, 128, 128, seed=7))
+    tr.set_params(VALUE, init_value(B, D, seed=8))
+    tr.iterate(its)
+    rng = tr.buffer(BUF_RNG).astype(np.int64)
+    m, a = 2147483647, 16807
+    base = 2 * N + 4 * T * N * its
+    want = np.array([x0 * pow(a, base + 4 * T * e, m) % m for e in range(N)],
+                    dtype=np.int64)
+    np.testing.assert_array_equal(rng, want)
