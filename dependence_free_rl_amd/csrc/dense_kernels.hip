@@ -49,17 +49,28 @@ struct RowsOnes {
 // observation::to_vector (bin_packing.h:31-40, generalised to D dims) of
 // row r: feature k = bin (k / 2D), c = k % 2D: c < D -> bins[bin][c] / 8,
 // else item[c - D] / 8.  Row r is slot s, env e with s * N + e = list[r]
-// (list == nullptr: slot `slot`, env r).
+// (list == nullptr: slot `slot`, env r).  With `action`, rows r >= term_from
+// are the terminal views E_t of transition q = r - term_from: the state of
+// slot t with bins[action[q]] -= item, taken before the reset (rl.h:336-343).
 struct ObsRows {
   EnvDesc E;
   const int8_t *bins, *items;
   const int *list;
   int N, slot;
+  const int32_t *action;
+  int term_from;
   __device__ float feature(int r, int k) const {
-    const int idx = list ? list[r] : slot * N + r;
     const int D = E.D, bin = k / (2 * D), c = k - bin * 2 * D;
-    const int v = c < D ? bins[(size_t)idx * E.B * D + bin * D + c]
-                        : items[(size_t)idx * 4 + c - D];
+    int idx, sub = -1;
+    if (action && r >= term_from) {
+      idx = r - term_from;
+      sub = action[idx];
+    } else {
+      idx = list ? list[r] : slot * N + r;
+    }
+    int v = c < D ? bins[(size_t)idx * E.B * D + bin * D + c]
+                  : items[(size_t)idx * 4 + c - D];
+    if (c < D && bin == sub) v -= items[(size_t)idx * 4 + c];
     return (float)v * (1.0f / (float)kCapacity);
   }
 };
@@ -192,7 +203,7 @@ hipError_t gemm(LA la, LB lb, EP ep, int M, int N, int K, const int *rows,
 
 }  // namespace dense
 
-// ----------------------------------------------------- full-MLP policy ----
+// ------------------------------------------------- full MLPs (pg, value) --
 // Layer l of a full MLP whose flat parameters follow model::parameters()
 // (nn.h:499-508): widths w[0] = input, ..., w[L] = output.
 static int layer_offset(const int *w, int l) {
@@ -217,6 +228,8 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
       la.list = a.list;
       la.N = a.N;
       la.slot = a.slot;
+      la.action = a.action;
+      la.term_from = a.term_from;
       e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
     } else {
       RowMajor la{a.act[l - 1], in};
@@ -244,6 +257,8 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
       lb.list = a.list;
       lb.N = a.N;
       lb.slot = a.slot;
+      lb.action = a.action;
+      lb.term_from = a.term_from;
       lb.ncol = in;
       e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
                splits, s);

@@ -100,21 +100,14 @@ struct EndListArgs {
   int *n_open;           // scalar: envs whose last step is not terminal
 };
 
+// TD targets and GAE around the value net (the net itself runs on the Dense
+// GEMMs, MlpArgs).
 struct ValueArgs {
   EnvDesc env;
   Batch b;
-  const float *params;   // flat value params
-  const float *w1t;      // [Fin][V1] transposed copy of W1 (row per feature)
   float *v_state;        // [T+1][N]   V(S_t)
   float *v_term;         // [T][N]     V(E_t) (terminal view of step t)
-  int with_term;         // eval: also evaluate the terminal views
-  // value-step row buffers (train mode)
-  const float *targets;  // [T][N]
-  float *row_g;          // [T*N]       V - target
-  float *row_h1;         // [T*N][V1]   post-relu layer-1 activations
-  float *row_h2;         // [T*N][V2]
-  float *row_d1;         // [T*N][V1]   dL/d(pre-act layer 1)
-  float *row_d2;         // [T*N][V2]
+  float *row_g;          // [T*N] dL/dV = V - target (targets kernel), or null
 };
 
 // Deterministic (argmax) evaluation, policy_gradient_deterministic_policy
@@ -166,6 +159,8 @@ struct MlpArgs {
   const int8_t *bins, *items;  // Batch state layout
   const int *list;             // row -> slot * N + env (nullptr: env = row)
   int N, slot;                 // slot used when list == nullptr
+  const int32_t *action;       // non-null: rows >= term_from are the terminal
+  int term_from;               //   views E_t of transition row - term_from
   const int *rows;             // device row count (nullptr: max_rows)
   int max_rows;
   int nlayers;
@@ -242,18 +237,10 @@ hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
 int rollout_grid(int B, int D, int H1, int H2);
 
 bool value_shape_supported(int V1, int V2);
-hipError_t launch_value_eval(const ValueArgs &a, int V1, int V2,
-                             hipStream_t s);
-hipError_t launch_value_rows(const ValueArgs &a, int V1, int V2,
-                             hipStream_t s);
-hipError_t launch_value_wgrad(const ValueArgs &a, int V1, int V2, float *slab,
-                              int slab_stride, int grid, hipStream_t s);
 hipError_t launch_value_targets(const ValueArgs &a, float gamma, float *targets,
                                 hipStream_t s);
 hipError_t launch_gae(const ValueArgs &a, float gamma, float lambda, float *adv,
                       hipStream_t s);
-hipError_t launch_transpose(const float *src, float *dst, int rows, int cols,
-                            hipStream_t s);
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s);
 hipError_t launch_sgd(float *params, const float *grad, int n, float lr,

@@ -121,11 +121,12 @@ struct xh_trainer {
   uint8_t *done = nullptr;
   uint32_t *rng = nullptr;
   // parameters and learner buffers
-  float *pp = nullptr, *vp = nullptr, *vw1t = nullptr;
+  float *pp = nullptr, *vp = nullptr;
   float *v_state = nullptr, *v_state0 = nullptr, *v_term = nullptr;
   float *targets = nullptr, *adv = nullptr;
-  float *row_g = nullptr, *row_h1 = nullptr, *row_h2 = nullptr,
-        *row_d1 = nullptr, *row_d2 = nullptr;
+  float *row_g = nullptr;               // [T*N] dL/dV of the value step
+  float *vact[2] = {nullptr, nullptr};  // value layer 1 / 2 outputs
+  float *vgr[2] = {nullptr, nullptr};   // their dL/d(pre-activation)
   float *pslab = nullptr, *vslab = nullptr;
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
@@ -179,16 +180,9 @@ struct xh_trainer {
     xh::ValueArgs a{};
     a.env = env;
     a.b = batch();
-    a.params = vp;
-    a.w1t = vw1t;
     a.v_state = v_state;
     a.v_term = v_term;
-    a.targets = targets;
     a.row_g = row_g;
-    a.row_h1 = row_h1;
-    a.row_h2 = row_h2;
-    a.row_d1 = row_d1;
-    a.row_d2 = row_d2;
     return a;
   }
   size_t N() const { return (size_t)cfg.num_envs; }
@@ -426,13 +420,6 @@ int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
   });
 }
 
-int refresh_value_transpose(xh_trainer *t) {
-  return timed(t, "value", [&]() {
-    return xh::launch_transpose(t->vp + t->vl.oW1(), t->vw1t, t->vl.V1,
-                                t->vl.Fin, t->ctx->stream);
-  });
-}
-
 int do_pg_rollout(xh_trainer *t);
 int do_pg_learn(xh_trainer *t);
 
@@ -467,26 +454,51 @@ int do_rollout(xh_trainer *t) {
   return XH_OK;
 }
 
+// The value net (full_layer Fin -> V1 -> V2 -> 1, ppo_training.cc:19-26) as a
+// Dense MLP over `rows` rows: S_0..S_T (row = slot * N + env), then the
+// terminal views E_t of transition row - N(T+1).  `out` receives V.
+xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
+  xh::MlpArgs m{};
+  m.env = t->env;
+  m.bins = t->bins;
+  m.items = t->items;
+  m.N = (int)t->N();
+  m.action = t->action;
+  m.term_from = (int)((t->T() + 1) * t->N());
+  m.max_rows = rows;
+  m.nlayers = 3;
+  m.w[0] = t->vl.Fin;
+  m.w[1] = t->vl.V1;
+  m.w[2] = t->vl.V2;
+  m.w[3] = 1;
+  m.params = t->vp;
+  m.act[0] = t->vact[0];
+  m.act[1] = t->vact[1];
+  m.act[2] = out;
+  m.grad[0] = t->vgr[0];
+  m.grad[1] = t->vgr[1];
+  m.grad[2] = t->row_g;
+  return m;
+}
+
 int do_learn(xh_trainer *t) {
   if (t->cfg.algo == XH_PG) return do_pg_learn(t);
   hipStream_t s = t->ctx->stream;
   const xh_config &c = t->cfg;
   xh::ValueArgs va = t->vargs();
-  // update_value_model (policy_gradient.h:196-218)
+  const int NS = (int)((t->T() + 1) * t->N()), NT = (int)(t->T() * t->N());
+  // update_value_model (policy_gradient.h:196-218): V over S_0..S_T and the
+  // terminal views E_t in one batch, TD targets and dL/dV = V - target on the
+  // transition rows (end rows have zero gradient), backward, one step
+  xh::MlpArgs vm = value_mlp(t, NS + NT, t->v_state0);
+  CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
   va.v_state = t->v_state0;
-  va.with_term = 1;
-  CHK(timed(t, "value", [&]() {
-    return xh::launch_value_eval(va, c.value_h1, c.value_h2, s);
-  }));
   CHK(timed(t, "value", [&]() {
     return xh::launch_value_targets(va, c.gamma, t->targets, s);
   }));
+  vm.max_rows = NT;
   CHK(timed(t, "value", [&]() {
-    return xh::launch_value_rows(va, c.value_h1, c.value_h2, s);
-  }));
-  CHK(timed(t, "value", [&]() {
-    return xh::launch_value_wgrad(va, c.value_h1, c.value_h2, t->vslab,
-                                  t->vslab_stride, t->vslab_n, s);
+    return xh::mlp_backward(vm, t->vslab, t->vslab_stride, t->vslab_n, s);
   }));
   CHK(timed(t, "reduce_sgd", [&]() {
     return xh::launch_slab_reduce(t->vslab, t->vslab_n, t->vslab_stride, t->nv,
@@ -494,13 +506,13 @@ int do_learn(xh_trainer *t) {
   }));
   CHK(allreduce(t, t->vgrad, t->nv));
   CHK(opt_apply(t, XH_VALUE, t->vp, t->vgrad, t->nv));
-  CHK(refresh_value_transpose(t));
-  // calculate_advantage (policy_gradient.h:220-281): post-update values
+  // calculate_advantage (policy_gradient.h:220-281) on post-update values;
+  // GAE zeroes V(terminal), the targets above used V(E_t)
+  vm.max_rows = NS;
+  vm.act[2] = t->v_state;
+  CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
   va.v_state = t->v_state;
-  va.with_term = 0;  // GAE zeroes V(terminal); keep eval-1 V(E_t) for targets
-  CHK(timed(t, "value", [&]() {
-    return xh::launch_value_eval(va, c.value_h1, c.value_h2, s);
-  }));
+  va.row_g = nullptr;
   CHK(timed(t, "value", [&]() {
     return xh::launch_gae(va, c.gamma, c.lambda, t->adv, s);
   }));
@@ -980,17 +992,17 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->rng, N * 4);
     A(&t->pp, (size_t)t->np * 4);
     A(&t->vp, (size_t)t->nv * 4);
-    A(&t->vw1t, (size_t)t->vl.V1 * t->vl.Fin * 4);
     A(&t->v_state, (T + 1) * N * 4);
-    A(&t->v_state0, (T + 1) * N * 4);
-    A(&t->v_term, T * N * 4);
+    // V(S_0..S_T) then V(E_0..E_{T-1}): one forward batch, v_term aliases
+    A(&t->v_state0, (2 * T + 1) * N * 4);
+    if (st == XH_OK) t->v_term = t->v_state0 + (T + 1) * N;
     A(&t->targets, T * N * 4);
     A(&t->adv, T * N * 4);
     A(&t->row_g, T * N * 4);
-    A(&t->row_h1, T * N * c.value_h1 * 4);
-    A(&t->row_h2, T * N * c.value_h2 * 4);
-    A(&t->row_d1, T * N * c.value_h1 * 4);
-    A(&t->row_d2, T * N * c.value_h2 * 4);
+    A(&t->vact[0], (2 * T + 1) * N * c.value_h1 * 4);
+    A(&t->vact[1], (2 * T + 1) * N * c.value_h2 * 4);
+    A(&t->vgr[0], T * N * c.value_h1 * 4);
+    A(&t->vgr[1], T * N * c.value_h2 * 4);
     t->rgrid = xh::rollout_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
     t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
     const int groups = (int)(T * N / (size_t)G);
@@ -1087,7 +1099,6 @@ int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
     float *dst = which == XH_POLICY ? t->pp : t->vp;
     HIPCHK(hipMemcpyAsync(dst, host, n * 4, hipMemcpyHostToDevice,
                           t->ctx->stream));
-    if (which == XH_VALUE) CHK(refresh_value_transpose(t));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     return XH_OK;
   });
