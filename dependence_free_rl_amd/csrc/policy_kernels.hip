@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         t1 = mfma32(wa, xb[s], t1);
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t1[j] = t1[j] > 0.0f ? t1[j] : 0.0f;
+      for (int j = 0; j < 16; ++j) t1[j] = relu(t1[j]);
       if (write_h1 && it == q) {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
