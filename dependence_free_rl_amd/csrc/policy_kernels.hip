@@ -175,8 +175,8 @@ __device__ __forceinline__ void layer1(const RowRaw<S> &rr, const float *lds,
       for (int u = 0; u < 4; ++u) {
         const float v0 = acc0[4 * q + u] + bq[u];
         const float v1 = acc1[4 * q + u] + bq[u];
-        acc0[4 * q + u] = v0 > 0.0f ? v0 : 0.0f;
-        acc1[4 * q + u] = v1 > 0.0f ? v1 : 0.0f;
+        acc0[4 * q + u] = relu(v0);
+        acc1[4 * q + u] = relu(v1);
       }
     }
     h1[it][0] = acc0;
@@ -234,7 +234,7 @@ __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
     const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float v = pre[4 * q + u] > 0.0f ? pre[4 * q + u] : 0.0f;
+      const float v = relu(pre[4 * q + u]);
       zp += v * wq[u];
     }
   }
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
           for (int u = 0; u < 4; ++u) {
             const int j = 4 * qq + u;
             const float v = pre[q][j];
-            const float h2 = v > 0.0f ? v : 0.0f;
+            const float h2 = relu(v);
             accW3[j] += gr * h2;
             const float d = v > 0.0f ? gr * wq[u] : 0.0f;
             accB2[j] += d;
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
           for (int u = 0; u < 4; ++u) {
             const int j = 4 * qq + u;
             const float v = pre[j];
-            accW3[j] += gr * (v > 0.0f ? v : 0.0f);
+            accW3[j] += gr * relu(v);
             const float d = v > 0.0f ? gr * wq[u] : 0.0f;
             accB2[j] += d;
             DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
