@@ -38,4 +38,9 @@ rc=$?; [ $rc -ne 0 ] && { tail -5 $O/prof_write.log; exit $rc; }
 PROFILE_OUT=$O/profiles python tools/pmc_summary.py $TAG $O/prof_trace $O/prof_fetch $O/prof_write \
     > $O/pmc_summary.log 2>&1
 rc=$?; cat $O/pmc_summary.log | head -20
+[ $rc -ne 0 ] && exit $rc
+# bench again with this pass's HBM counters in profiles/ (roofline.traffic)
+cp $O/profiles/${TAG}_pmc_summary.json profiles/ &&
+timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > $O/bench_final.log 2>&1
+rc=$?; tail -1 $O/bench_final.log | cut -c1-2000
 exit $rc
