@@ -22,6 +22,8 @@
 #include "xh_device.h"
 #include "xh_kernels.h"
 
+#include <cstdlib>
+
 namespace xh {
 
 template <int B_, int D_, int H1_, int H2_>
@@ -241,6 +243,62 @@ __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
   return zp + __shfl_xor(zp, 32, kWave);
 }
 
+// Softmax of the candidate-bin scores z (lane = row = bin of env `env`,
+// whose B rows sit in lanes seg0 ..), the categorical sample (or the forced
+// action), and the env transition into slot t+1 (rl.h:325-349,
+// bin_packing.h:53-79).  `cur` holds this lane's raw row (rows lr / 32+lr).
+template <class S>
+__device__ __forceinline__ void sample_step(const RolloutArgs &a, float z,
+                                            int env, int seg0, int bin,
+                                            const RowRaw<S> &cur) {
+  constexpr int B = S::B;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int N = a.b.N, t = a.t;
+  const float ex = expf(z);
+  const float sum = seg_sum<B>(ex);
+  const float p = ex / sum;
+  if (a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
+  if (a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
+  if (a.qold_out) a.qold_out[((size_t)t * N + env) * B + bin] = p;
+
+  uint32_t x = a.b.rng[env];
+  int choice;
+  if (a.forced) {
+    choice = a.forced[(size_t)t * N + env];
+    (void)canonical(x);  // the sampler's two engine draws
+  } else {
+    choice = sample_discrete<B>(p, lane, canonical(x));
+  }
+  const float pold = wave_shfl(p, seg0 + choice);
+
+  // this lane's row (= lane) is row (h ? 32 : 0) + lr of the prefetch
+  int nb[S::D];
+  int neg = 0;
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) {
+    const int bv = h ? cur.bv[1][d] : cur.bv[0][d];
+    const int iv = h ? cur.iv[1][d] : cur.iv[0][d];
+    nb[d] = bin == choice ? bv - iv : bv;
+    neg |= nb[d] < 0;
+  }
+  const int done = __shfl(neg, seg0 + choice, kWave);
+  // apply -> get_item, or game over -> reset -> get_item: 2 draws either way
+  const bool first = canonical(x) < a.env.p_a;
+  int8_t *ob = a.b.bins + ((size_t)(t + 1) * N + env) * S::BD + bin * S::D;
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) ob[d] = (int8_t)(done ? kCapacity : nb[d]);
+  if (bin == 0) {
+    int8_t *oi = a.b.items + ((size_t)(t + 1) * N + env) * 4;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+    a.b.action[(size_t)t * N + env] = choice;
+    a.b.pold[(size_t)t * N + env] = pold;
+    a.b.done[(size_t)t * N + env] = (uint8_t)done;
+    a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
+  }
+}
+
 // =========================================================== rollout step ==
 template <class S>
 __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
@@ -284,52 +342,97 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
 #pragma unroll
       for (int o = 0; o < S::NOT; ++o) zs += lds[S::L_Z + o * 64 + lane];
       const float z = zs + lds[S::L_B3];
-      const float ex = expf(z);
-      const float sum = seg_sum<B>(ex);
-      const float p = ex / sum;
-      if (a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
-      if (a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
-      if (a.qold_out) a.qold_out[((size_t)t * N + env) * B + bin] = p;
-
-      uint32_t x = a.b.rng[env];
-      int choice;
-      if (a.forced) {
-        choice = a.forced[(size_t)t * N + env];
-        (void)canonical(x);  // the sampler's two engine draws
-      } else {
-        choice = sample_discrete<B>(p, lane, canonical(x));
-      }
-      const float pold = wave_shfl(p, seg0 + choice);
-
-      // this lane's row (= lane) is row (h ? 32 : 0) + lr of the prefetch
-      int nb[S::D];
-      int neg = 0;
-#pragma unroll
-      for (int d = 0; d < S::D; ++d) {
-        const int bv = h ? cur.bv[1][d] : cur.bv[0][d];
-        const int iv = h ? cur.iv[1][d] : cur.iv[0][d];
-        nb[d] = bin == choice ? bv - iv : bv;
-        neg |= nb[d] < 0;
-      }
-      const int done = __shfl(neg, seg0 + choice, kWave);
-      // apply -> get_item, or game over -> reset -> get_item: 2 draws either way
-      const bool first = canonical(x) < a.env.p_a;
-      int8_t *ob = a.b.bins + ((size_t)(t + 1) * N + env) * S::BD + bin * S::D;
-#pragma unroll
-      for (int d = 0; d < S::D; ++d) ob[d] = (int8_t)(done ? kCapacity : nb[d]);
-      if (bin == 0) {
-        int8_t *oi = a.b.items + ((size_t)(t + 1) * N + env) * 4;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-          oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
-        a.b.action[(size_t)t * N + env] = choice;
-        a.b.pold[(size_t)t * N + env] = pold;
-        a.b.done[(size_t)t * N + env] = (uint8_t)done;
-        a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
-      }
+      sample_step<S>(a, z, env, seg0, bin, cur);
     }
     __syncthreads();
     cur = nxt;
+  }
+}
+
+// ================================================ rollout step, wave per env ==
+// B = 64, [128,128] (config 3): one wave per env.  The wave runs all four H2
+// tiles itself (layer 1 recomputed per tile, as each of rollout_step_kernel's
+// four waves does), keeps the partial logits in registers and samples its own
+// env, so no barrier separates the forward from the sampler and, at four
+// waves per SIMD, one wave's softmax / double-precision sampling / env update
+// issues beside the other waves' MFMAs.  Every operation and its order match
+// rollout_step_kernel (layer1, layer2, logit_part, the o-ordered logit sum),
+// so logits, probabilities and actions are bit-identical.
+template <class S>
+__global__ __launch_bounds__(512, 4) void rollout_wave_kernel(RolloutArgs a) {
+  static_assert(S::B == 64 && S::NIT == 4 && S::NOT == 4, "wave rollout: B=64, [128,128]");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int wpb = blockDim.x >> 6;
+  for (int env = blockIdx.x * wpb + w; env < a.b.N; env += gridDim.x * wpb) {
+    RowRaw<S> cur;
+    fetch_rows<S>(a.b, a.t, env, cur);
+    float xb[2][S::S1];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
+    float zl[2] = {0.0f, 0.0f};  // partial logit sums of rows lr / 32 + lr
+#pragma unroll 1
+    for (int o2t = 0; o2t < 4; ++o2t) {
+      const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
+      f32x16 pre[2];
+      pre[0] = zero16();
+      pre[1] = zero16();
+#pragma unroll 1
+      for (int it = 0; it < 4; ++it) {
+        // layer-1 tile it, exactly as layer1(): chain, + bias, relu
+        f32x16 t1[2];
+        t1[0] = zero16();
+        t1[1] = zero16();
+#pragma unroll
+        for (int s = 0; s < S::S1; ++s) {
+          const int k = 2 * s + h;
+          const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+          t1[0] = mfma32(wa, xb[0][s], t1[0]);
+          t1[1] = mfma32(wa, xb[1][s], t1[1]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * q + 4 * h);
+          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            t1[0][4 * q + u] = relu(t1[0][4 * q + u] + bq[u]);
+            t1[1][4 * q + u] = relu(t1[1][4 * q + u] + bq[u]);
+          }
+        }
+        // layer 2 k-steps of tile it, exactly as layer2<S, 2>()
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 a4 = lds4(wrow + it * 32 + 8 * q);
+          const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            pre[0] = mfma32(av[u], t1[0][4 * q + u], pre[0]);
+            pre[1] = mfma32(av[u], t1[1][4 * q + u], pre[1]);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = lds4(lds + S::L_B2 + o2t * 32 + 8 * q + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          pre[0][4 * q + u] += bq[u];
+          pre[1][4 * q + u] += bq[u];
+        }
+      }
+      zl[0] += logit_part<S>(lds, pre[0], o2t);
+      zl[1] += logit_part<S>(lds, pre[1], o2t);
+    }
+    // lane = row = bin: rows 0..31 in lane half 0, 32..63 in half 1
+    const float z = (h ? zl[1] : zl[0]) + lds[S::L_B3];
+    sample_step<S>(a, z, env, 0, lane, cur);
   }
 }
 
@@ -1344,6 +1447,13 @@ constexpr size_t train_lds() {
          (S::L_TRAIN_END > S::L_TRAIN8_END ? S::L_TRAIN_END : S::L_TRAIN8_END);
 }
 
+// XH_ROLLOUT_KERNEL=4 keeps the 4-wave rollout where the wave-per-env kernel
+// would run (A/B measurements and the bit-identity test); read per launch.
+static bool rollout4() {
+  const char *e = std::getenv("XH_ROLLOUT_KERNEL");
+  return e && std::atoi(e) == 4;
+}
+
 bool policy_shape_supported(int B, int D, int H1, int H2) {
 #define X(XB, XD, XH1, XH2) \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) return true;
@@ -1393,6 +1503,22 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
       attr = true;                                                           \
     }                                                                        \
     const int ng = a.b.N / S::G;                                             \
+    if constexpr (S::B == 64 && S::NIT == 4 && S::NOT == 4) {                \
+      if (!rollout4()) {                                                     \
+        static bool wattr = false;                                           \
+        if (!wattr) {                                                        \
+          (void)hipFuncSetAttribute((const void *)rollout_wave_kernel<S>,    \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                    (int)rollout_lds<S>());                  \
+          wattr = true;                                                      \
+        }                                                                    \
+        const int wg = (ng + 7) / 8;                                         \
+        hipLaunchKernelGGL(rollout_wave_kernel<S>,                           \
+                           dim3(grid < wg ? grid : wg), dim3(512),           \
+                           rollout_lds<S>(), s, a);                          \
+        return hipGetLastError();                                            \
+      }                                                                      \
+    }                                                                        \
     if constexpr (S::HG == 1)                                                \
       hipLaunchKernelGGL(rollout_step_kernel<S>, dim3(grid < ng ? grid : ng),\
                          dim3(256), rollout_lds<S>(), s, a);                 \

@@ -155,3 +155,36 @@ def test_c3_rng_positions_full_size(ctx):
     want = np.array([x0 * pow(a, base + 4 * T * e, m) % m for e in range(N)],
                     dtype=np.int64)
     np.testing.assert_array_equal(rng, want)
+
+
+def test_wave_rollout_matches_4wave(ctx, monkeypatch):
+    """Full config-3 size: the wave-per-env rollout (default at B=64,
+    [128,128]) and the 4-wave rollout (XH_ROLLOUT_KERNEL=4) produce
+    the same trajectories (actions, states, items, dones) and RNG states on
+    the same parameters (T = 4 steps of 32768 envs); logits / probabilities
+    agree to the last place."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
+                                                BUF_ITEMS, BUF_LOGITS, BUF_POLD,
+                                                BUF_PROBS, BUF_RNG)
+    N, B, D, T = 32768, 64, 2, 4
+    pp, vp = init_policy(D, 128, 128, seed=11), init_value(B, D, seed=12)
+    bufs = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_LOGITS, BUF_POLD,
+            BUF_PROBS, BUF_RNG)
+    got = {}
+    for kern in ("wave", "4"):
+        if kern == "4":
+            monkeypatch.setenv("XH_ROLLOUT_KERNEL", "4")
+        tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T,
+                     widths=(128, 128), rng_state=99)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        tr.rollout()
+        got[kern] = [tr.buffer(b).copy() for b in bufs]
+    exact = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_RNG)
+    for b, x, y in zip(bufs, got["wave"], got["4"]):
+        if b in exact:
+            np.testing.assert_array_equal(x, y, err_msg="buffer %d" % b)
+        else:  # ~0.03% of the logits differ in the last place
+            np.testing.assert_allclose(x, y, rtol=2e-6, atol=1e-7,
+                                       err_msg="buffer %d" % b)
