@@ -73,6 +73,7 @@ def _load():
         "xh_trainer_get_params": (i, [vp, i, vp, sz]),
         "xh_trainer_set_optimizer": (i, [vp, i, i, C.c_float, C.c_float,
                                          C.c_float, C.c_float]),
+        "xh_trainer_set_learning_rate": (i, [vp, i, C.c_float]),
         "xh_trainer_rollout": (i, [vp]),
         "xh_trainer_learn": (i, [vp]),
         "xh_trainer_iterate": (i, [vp, i]),

@@ -1154,6 +1154,19 @@ int xh_trainer_set_optimizer(xh_trainer *t, int which, int kind, float lr,
   });
 }
 
+int xh_trainer_set_learning_rate(xh_trainer *t, int which, float lr) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    if (which != XH_POLICY && which != XH_VALUE)
+      return fail(XH_ERR_INVALID, "learning rate: which %d", which);
+    if (which == XH_VALUE && t->cfg.algo == XH_PG)
+      return fail(XH_ERR_INVALID, "learning rate: REINFORCE has no value net");
+    t->opt[which].lr = lr;
+    (which == XH_POLICY ? t->cfg.lr_policy : t->cfg.lr_value) = lr;
+    return XH_OK;
+  });
+}
+
 int xh_trainer_rollout(xh_trainer *t) {
   return guard([&]() -> int {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");

@@ -224,6 +224,10 @@ class Trainer:
             self.h, which, _lib.OPTIMIZERS[kind], lr, weight_decay, beta1,
             beta2))
 
+    def set_learning_rate(self, which, lr):
+        """optimizer::set_rate (nn.h:591); the optimizer state is kept."""
+        check(_lib.lib.xh_trainer_set_learning_rate(self.h, which, lr))
+
     # -------------------------------------------------------------- loop --
     def rollout(self):
         check(_lib.lib.xh_trainer_rollout(self.h))

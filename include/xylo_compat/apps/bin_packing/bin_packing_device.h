@@ -256,6 +256,7 @@ class session {
     if (state_ != rolled)
       throw xeno::error("xylo-hip: learner.step() without new experience");
     push_params();
+    sync_rates();
     check(xh_trainer_learn(tr_->h), "xh_trainer_learn");
     state_ = idle;
     learned_unforgotten_ = true;
@@ -463,6 +464,22 @@ class session {
     upload_host_states();
     if (const char *p = std::getenv("XYLO_HIP_DUMP"))
       write_params(std::string(p) + ".policy.0.bin", XH_POLICY);
+  }
+
+  // optimizer::set_rate between steps (nn.h:591) reaches the device
+  void sync_rates() {
+    for (int which : {XH_POLICY, XH_VALUE}) {
+      xylo::optimizer *o = which == XH_POLICY ? learner_.action_optimizer
+                                              : learner_.value_optimizer;
+      if (!o) continue;
+      const float want = o->rate();
+      const float have = which == XH_POLICY ? tr_->cfg.lr_policy : tr_->cfg.lr_value;
+      if (want != have) {
+        check(xh_trainer_set_learning_rate(tr_->h, which, want),
+              "xh_trainer_set_learning_rate");
+        (which == XH_POLICY ? tr_->cfg.lr_policy : tr_->cfg.lr_value) = want;
+      }
+    }
   }
 
   void set_optimizers() {

@@ -123,6 +123,11 @@ enum { XH_OPT_SGD = 0, XH_OPT_MOMENTUM = 1, XH_OPT_ADAM = 2 };
 int xh_trainer_set_optimizer(xh_trainer *t, int which, int kind, float lr,
                              float weight_decay, float beta1, float beta2);
 
+/* optimizer::set_rate (nn.h:591): new learning rate for the policy / value
+ * optimizer from the next learn() on; its state (velocity, moments, adam's
+ * step counter) is kept. */
+int xh_trainer_set_learning_rate(xh_trainer *t, int which, float lr);
+
 /* One iteration's rollout: T steps of every env (one kernel per step). */
 int xh_trainer_rollout(xh_trainer *t);
 /* learn(): value step, advantages, `epochs` policy steps; then the batch's
