@@ -224,7 +224,7 @@ int timed(xh_trainer *t, const char *name, F &&launch) {
 }
 
 int allreduce(xh_trainer *t, float *buf, int n) {
-  if (t->ctx->world <= 1) return XH_OK;
+  if (!t->ctx->comm) return XH_OK;
   hipStream_t s = t->ctx->stream;
   return timed(t, "allreduce", [&]() -> hipError_t {
     ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum,
@@ -234,7 +234,7 @@ int allreduce(xh_trainer *t, float *buf, int n) {
 }
 
 int allreduce_d(xh_trainer *t, double *buf, int n) {
-  if (t->ctx->world <= 1) return XH_OK;
+  if (!t->ctx->comm) return XH_OK;
   hipStream_t s = t->ctx->stream;
   return timed(t, "allreduce", [&]() -> hipError_t {
     ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum,
@@ -840,7 +840,9 @@ int xh_ctx_create(int device, int rank, int world, const void *uid128,
       delete c;
       return fail(XH_ERR_HIP, "stream: %s", hipGetErrorString(e));
     }
-    if (world > 1) {
+    // a communicator for world > 1, and for world == 1 when a unique id is
+    // given (a one-rank RCCL comm: the multi-GPU code path on one device)
+    if (world > 1 || uid128) {
       if (!uid128) {
         (void)hipStreamDestroy(c->stream);
         delete c;
@@ -885,7 +887,7 @@ int xh_ctx_synchronize(xh_ctx *c) {
 int xh_ctx_allreduce_host(xh_ctx *c, float *data, size_t n) {
   return guard([&]() -> int {
     if (!c || (!data && n)) return fail(XH_ERR_INVALID, "null arg");
-    if (c->world <= 1 || n == 0) return XH_OK;
+    if (!c->comm || n == 0) return XH_OK;
     float *d = nullptr;
     HIPCHK(hipMalloc(&d, n * sizeof(float)));
     HIPCHK(hipMemcpyAsync(d, data, n * sizeof(float), hipMemcpyHostToDevice,

@@ -48,7 +48,9 @@ typedef struct xh_ctx xh_ctx;
 /* 128-byte RCCL unique id (ncclGetUniqueId) for a world > 1 job. */
 int xh_comm_unique_id(void *out128);
 /* device: HIP device ordinal; rank/world: this process in a one-process-per-
- * GPU job; uid128 (world > 1): the id from rank 0, broadcast by the caller. */
+ * GPU job; uid128 (required when world > 1): the id from rank 0, broadcast
+ * by the caller.  With world == 1 a non-null uid128 creates a one-rank RCCL
+ * communicator, so the all-reduce path runs on a single device too. */
 int xh_ctx_create(int device, int rank, int world, const void *uid128,
                   xh_ctx **out);
 int xh_ctx_destroy(xh_ctx *ctx);
