@@ -47,7 +47,7 @@ def cpu_baseline(seconds_budget=20.0):
     """Time the reference's single-threaded CPU path on a bounded sample of
     the same workload (64 bins, 2-D, [128,128], PPO k=4, T=4)."""
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    n_env, iters = 16, 20
+    n_env, iters = 16, 60  # ~4k env-steps: 10-20 s on one core
     sample = ("reference ppo_learner, %d envs x T=%d x %d iterations, B=64 D=2 "
               "[128,128], 1 thread" % (n_env, T, iters))
     if os.path.exists(harness):
