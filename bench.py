@@ -204,7 +204,8 @@ def main():
             "reduce_sgd": round(ms_r / args.steps, 3),
             "allreduce": round(ms_a / args.steps, 3)},
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    # the CPU baseline is timed on rank 0 of the N=1 run only
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(line), flush=True)
