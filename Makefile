@@ -29,7 +29,7 @@ REF_APPS := ppo_training ac_training ppo2_training pg_training deep_agent \
 EXAMPLES := $(patsubst examples/%.cc,$(COMPAT)/%,$(wildcard examples/*.cc))
 COMPAT_HDRS := $(shell find include/xylo_compat -name '*.h') include/xylo_hip.h
 
-.PHONY: all lib oracle compat clean
+.PHONY: all lib oracle compat clean diag
 all: lib oracle compat
 
 lib: $(LIB)
@@ -43,6 +43,15 @@ $(SRC)/xylo_hip.o: $(SRC)/xylo_hip.cpp $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl \
 	    -Wl,-rpath,/opt/rocm/lib
+
+# diagnostic library with the phase-ablation bits compiled in (tools/ablate.sh;
+# loaded through XH_LIB_PATH, never by the product path)
+DIAG := build/diag
+diag: $(OBJS)
+	@mkdir -p $(DIAG)
+	$(HIPCC) $(HIPFLAGS) -DXH_DIAG_ABLATE=1 -c $(SRC)/policy_kernels.hip -o $(DIAG)/policy_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(DIAG)/libxylo_hip.so $(DIAG)/policy_kernels.o \
+	    $(filter-out $(SRC)/policy_kernels.o,$(OBJS)) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle port

@@ -8,7 +8,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libxylo_hip.so")
+# XH_LIB_PATH: diagnostic builds only (`make diag`, tools/ablate.sh)
+LIB_PATH = os.environ.get("XH_LIB_PATH") or os.path.join(HERE, "libxylo_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "xylo_hip.h")
 
 XH_OK, XH_ERR_INVALID, XH_ERR_HIP, XH_ERR_RCCL, XH_ERR_STATE = range(5)

@@ -24,6 +24,12 @@
 
 #include <cstdlib>
 
+// Diagnostic builds only (make diag): extra XH_ABLATE bits in the 8-wave
+// train kernel that drop whole phases (results are wrong by design).
+#ifndef XH_DIAG_ABLATE
+#define XH_DIAG_ABLATE 0
+#endif
+
 namespace xh {
 
 template <int B_, int D_, int H1_, int H2_>
@@ -1296,6 +1302,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       f32x16 dh = zero16();
 #pragma unroll 8
       for (int s = 0; s < S::H2 / 2; ++s) {
+        if (XH_DIAG_ABLATE && (a.ablate & 16)) break;
         const int k = 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
                     DAT[k * S::TS + rt * 32 + lr], dh);
@@ -1320,6 +1327,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
 #pragma unroll
       for (int s4 = 0; s4 < 8; ++s4) {
+        if (XH_DIAG_ABLATE && (a.ablate & 32)) break;
         const float4 av = lds4(pa + 4 * s4);
         const float4 b0 = lds4(pb0 + 4 * s4);
         const float4 b1 = lds4(pb1 + 4 * s4);
