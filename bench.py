@@ -114,7 +114,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     uid = None
+    device = local
     if world > 1:
+        # one node by the bench contract: RCCL's bootstrap stays on loopback
+        # (the container hostname may not resolve); device = LOCAL_RANK, or
+        # modulo the visible devices if the launcher narrowed them per rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        import torch
+        ndev = torch.cuda.device_count()  # does not initialise the GPU
+        if ndev > 0 and local >= ndev:
+            device = local % ndev
         import torch.distributed as dist
         dist.init_process_group("gloo")
         from dependence_free_rl_amd import Context
@@ -124,7 +133,7 @@ def main():
 
     from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
                                         init_policy, init_value)
-    ctx = Context(device=local, rank=rank, world=world, uid=uid)
+    ctx = Context(device=device, rank=rank, world=world, uid=uid)
     n = args.envs
     tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=n, steps=T,
                  widths=(H1, H2), value_widths=(V1, V2), rng_state=20241008,
@@ -168,6 +177,14 @@ def main():
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
     alg_bytes = n * T * (B * D + 4 + 12) + 256 * 17344 * 4
     achieved = flops_epoch / (avg_ms * 1e-3) / 1e12
+    # whole-iteration HBM roofline (BASELINE metric: "fraction of the HBM
+    # roofline"): compulsory bytes per env-step, SURVEY §8d -- env state
+    # read + write (2*B*D int8) and one trajectory record (B*D state + D item
+    # + action, p_old, reward, V (4 B each) + done (1 B)) written once and read
+    # 3 + k times; params and slabs excluded.
+    rec = B * D + D + 4 * 4 + 1
+    hbm_bytes_per_step = 2 * B * D + rec * (1 + 3 + 4)
+    hbm_gbs = value * hbm_bytes_per_step / 1e9
     line = {
         "metric": "env-steps/sec (whole node) PPO bin-packing 64-bin",
         "value": round(value, 1),
@@ -197,6 +214,10 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
                      "flops_per_launch": flops_epoch},
+        "hbm_roofline": {"bytes_per_env_step": hbm_bytes_per_step,
+                         "achieved": round(hbm_gbs, 2),
+                         "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                         "frac": round(hbm_gbs / (HBM_PEAK_GBS * world), 6)},
         "phase_ms_per_step": {
             "rollout": round(ms_ro / args.steps, 3),
             "policy_train": round(ms_pt / args.steps, 3),
