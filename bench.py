@@ -7,7 +7,7 @@ policy [128,128], value [256,64,32], T=4, k=4 PPO epochs), weak-scaled over
 N GPUs (config 4 at N=8).  A "step" is one training iteration: T env steps
 of every env + learn() (value step, GAE, 4 policy epochs), i.e. N*T env-steps.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--config 2|3|5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
@@ -27,8 +27,34 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# BASELINE.json configs that run on the device (config 1 is the CPU-only
+# REINFORCE plumbing case; config 4 = config 3 per GPU at N=8).  The default
+# and headline is config 3; --config 2 / 5 measure the other shapes.
+CONFIGS = {
+    2: dict(algo="ppo", B=32, D=1, N=4096, T=4, H=(64, 64), epochs=4,
+            ref_iters=100,
+            name="PPO, 1-D bin packing 32 bins, %d envs/GPU, per-bin policy "
+                 "[64,64], value [64,64,32], T=4, k=4"),
+    3: dict(algo="ppo", B=64, D=2, N=32768, T=4, H=(128, 128), epochs=4,
+            ref_iters=60,
+            name="PPO, 2-D bin packing 64 bins, %d envs/GPU, per-bin policy "
+                 "[128,128], value [256,64,32], T=4, k=4"),
+    5: dict(algo="ac", B=128, D=3, N=16384, T=8, H=(128, 128), epochs=1,
+            ref_iters=20,
+            name="online actor-critic, 3-D bin packing 128 bins, %d envs/GPU, "
+                 "per-bin policy [128,128], value [768,64,32], T=8"),
+}
 B, D, T, H1, H2, V1, V2 = 64, 2, 4, 128, 128, 64, 32
 F0 = 2 * D
+ALGO, EPOCHS, REF_ITERS = "ppo", 4, 60
+
+
+def select_config(c):
+    global B, D, T, H1, H2, F0, ALGO, EPOCHS, REF_ITERS
+    k = CONFIGS[c]
+    B, D, T, (H1, H2) = k["B"], k["D"], k["T"], k["H"]
+    F0, ALGO, EPOCHS, REF_ITERS = 2 * D, k["algo"], k["epochs"], k["ref_iters"]
+    return k
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 HBM_PEAK_GBS = 8000.0
 
@@ -47,13 +73,15 @@ def cpu_baseline(seconds_budget=20.0):
     """Time the reference's single-threaded CPU path on a bounded sample of
     the same workload (64 bins, 2-D, [128,128], PPO k=4, T=4)."""
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    n_env, iters = 16, 60  # ~4k env-steps: 10-20 s on one core
-    sample = ("reference ppo_learner, %d envs x T=%d x %d iterations, B=64 D=2 "
-              "[128,128], 1 thread" % (n_env, T, iters))
+    n_env, iters = 16, REF_ITERS  # 10-20 s on one core
+    learner = "ppo_learner" if ALGO == "ppo" else "actor_critic_learner"
+    sample = ("reference %s, %d envs x T=%d x %d iterations, B=%d D=%d "
+              "[%d,%d], 1 thread" % (learner, n_env, T, iters, B, D, H1, H2))
     if os.path.exists(harness):
         try:
             out = subprocess.run(
-                [harness, "bench", "algo=ppo", "B=64", "D=2", "widths=128,128",
+                [harness, "bench", "algo=%s" % ALGO, "B=%d" % B, "D=%d" % D,
+                 "widths=%d,%d" % (H1, H2),
                  "N=%d" % n_env, "T=%d" % T, "iters=%d" % iters, "seed=1"],
                 capture_output=True, text=True, timeout=600, check=True)
             r = json.loads(out.stdout.strip().splitlines()[-1])
@@ -66,9 +94,11 @@ def cpu_baseline(seconds_budget=20.0):
     from oracle import pyoracle as po
     from dependence_free_rl_amd.trainer import init_policy, init_value
     n_env, iters = 8, 3
-    pol = po.perbin_model(F0, [H1, H2], po.OR_SOFTMAX)
+    pol = po.perbin_model(F0, [H1, H2],
+                          po.OR_SOFTMAX if ALGO == "ppo" else po.OR_SOFTMAX_XENT)
     val = po.full_model(B * F0, [V1, V2], 1)
-    tr = po.Trainer(po.OR_PPO, B, D, n_env, T, pol, init_policy(D, H1, H2),
+    tr = po.Trainer(po.OR_PPO if ALGO == "ppo" else po.OR_AC, B, D, n_env, T,
+                    pol, init_policy(D, H1, H2),
                     val, init_value(B, D), x0=1)
     t0 = time.perf_counter()
     for _ in range(iters):
@@ -94,7 +124,10 @@ def pmc_traffic(kernel="policy_train"):
     with open(files[-1]) as f:
         summ = json.load(f)
     # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
-    s = next((v for k, v in sorted(summ.items()) if k.startswith(kernel)), None)
+    # only a summary of this very shape counts (PShape<B, D, H1, H2>)
+    shape = "PShape<%d, %d, %d, %d>" % (B, D, H1, H2)
+    s = next((v for k, v in sorted(summ.items())
+              if k.startswith(kernel) and shape in v.get("kernel", "")), None)
     if not s:
         return None, None
     return s["hbm_bytes"], os.path.relpath(files[-1], REPO)
@@ -105,9 +138,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                    help="BASELINE.json config (3 = the headline)")
+    ap.add_argument("--envs", type=int, default=None,
+                    help="envs per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    cfg = select_config(args.config)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -134,8 +171,8 @@ def main():
     from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
                                         init_policy, init_value)
     ctx = Context(device=device, rank=rank, world=world, uid=uid)
-    n = args.envs
-    tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=n, steps=T,
+    n = args.envs or cfg["N"]
+    tr = Trainer(ctx, algo=ALGO, bins=B, dims=D, num_envs=n, steps=T,
                  widths=(H1, H2), value_widths=(V1, V2), rng_state=20241008,
                  num_envs_global=n * world, env_offset=n * rank)
     # random-init weights of the reference architecture (same on every rank)
@@ -175,7 +212,8 @@ def main():
     traffic, traffic_src = pmc_traffic()
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
-    alg_bytes = n * T * (B * D + 4 + 12) + 256 * 17344 * 4
+    from dependence_free_rl_amd.trainer import policy_param_count
+    alg_bytes = n * T * (B * D + 4 + 12) + 256 * policy_param_count(D, H1, H2) * 4
     achieved = flops_epoch / (avg_ms * 1e-3) / 1e12
     # whole-iteration HBM roofline (BASELINE metric: "fraction of the HBM
     # roofline"): compulsory bytes per env-step, SURVEY §8d -- env state
@@ -183,10 +221,17 @@ def main():
     # + action, p_old, reward, V (4 B each) + done (1 B)) written once and read
     # 3 + k times; params and slabs excluded.
     rec = B * D + D + 4 * 4 + 1
-    hbm_bytes_per_step = 2 * B * D + rec * (1 + 3 + 4)
+    hbm_bytes_per_step = 2 * B * D + rec * (1 + 3 + EPOCHS)
     hbm_gbs = value * hbm_bytes_per_step / 1e9
+    if args.config == 3:
+        metric = "env-steps/sec (whole node) PPO bin-packing 64-bin"
+        workload = "BASELINE config %d: " % (3 if world == 1 else 4)
+    else:
+        metric = "env-steps/sec (whole node) %s bin-packing %d-bin %d-D" % (
+            "PPO" if ALGO == "ppo" else "actor-critic", B, D)
+        workload = "BASELINE config %d: " % args.config
     line = {
-        "metric": "env-steps/sec (whole node) PPO bin-packing 64-bin",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -199,12 +244,9 @@ def main():
         "dtype": "f32",
         "data": "synthetic (fixed-size bin-packing instances, random-init "
                 "weights of the reference architecture)",
-        "config": {"workload": "BASELINE config %d: PPO, 2-D bin packing 64 "
-                               "bins, %d envs/GPU, per-bin policy [128,128], "
-                               "value [256,64,32], T=4, k=4"
-                               % (3 if world == 1 else 4, n),
+        "config": {"workload": workload + cfg["name"] % n,
                    "envs_per_gpu": n, "bins": B, "dims": D, "T": T,
-                   "epochs": 4, "parallelism": "dp%d" % world},
+                   "epochs": EPOCHS, "parallelism": "dp%d" % world},
         "roofline": {"kernel": "policy_train", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s",
