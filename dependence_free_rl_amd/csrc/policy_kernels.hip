@@ -231,7 +231,12 @@ __device__ __forceinline__ void layer2(const float *lds,
 }
 
 // Partial logit over this tile's 32 H2 units for row rt*32 + (lane&31).
-template <class S>
+// kSwap: the lane-half exchange as v_permlane32_swap (a volatile asm, which
+// the scheduler cannot move MFMAs across: only for the train kernel's
+// serial logit phase; inside the rollout's MFMA streams the ds_bpermute
+// keeps the schedule, measured 2.44 vs 2.59 ms per iteration).  Both give
+// the same bits (zp_lo + zp_hi in either half).
+template <class S, bool kSwap = false>
 __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
                                             int o2t) {
   const int h = (threadIdx.x & 63) >> 5;
@@ -246,7 +251,7 @@ __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
       zp += v * wq[u];
     }
   }
-  return zp + __shfl_xor(zp, 32, kWave);
+  return zp + (kSwap ? half_swap(zp) : __shfl_xor(zp, 32, kWave));
 }
 
 // Softmax of the candidate-bin scores z (lane = row = bin of env `env`,
@@ -1208,7 +1213,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     for (int hg = 0; hg < HG; ++hg) {
       if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
       pre = forward(HG == 1);
-      const float zp = logit_part<S>(lds, pre, q);
+      const float zp = logit_part<S, true>(lds, pre, q);
       if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
     }
     __syncthreads();
@@ -1237,10 +1242,15 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const int seg0 = (lane / SEG) * SEG;
       // p of the chosen bin (bin c lives in lane c % 64 of row block c / 64)
       float pc = 0.0f;
+      if constexpr (B == 64) {  // one env per wave: c is wave-uniform
+        const int cu = __builtin_amdgcn_readfirstlane(c);
+        pc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[0]), cu));
+      } else {
 #pragma unroll
-      for (int k = 0; k < HG; ++k) {
-        const float v = wave_shfl(p[k], seg0 + (c % SEG));
-        if (HG == 1 || c / 64 == k) pc = v;
+        for (int k = 0; k < HG; ++k) {
+          const float v = wave_shfl(p[k], seg0 + (c % SEG));
+          if (HG == 1 || c / 64 == k) pc = v;
+        }
       }
 #pragma unroll
       for (int k = 0; k < HG; ++k) {
@@ -1280,7 +1290,9 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       }
       // ---- backward through layer 3 and the layer-2 relu
       {
-        const float gr = wave_shfl(gzk[hg], rt * 32 + lr);
+        // row rt*32 + lr's gradient: own lane in half rt, else lane ^ 32
+        const float sw = half_swap(gzk[hg]);
+        const float gr = h == rt ? gzk[hg] : sw;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);

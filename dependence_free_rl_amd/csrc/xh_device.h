@@ -76,11 +76,52 @@ __device__ __forceinline__ double wave_shfl_d(double v, int src) {
   return __shfl(v, src, kWave);
 }
 
-// Sum over aligned segments of S lanes (S a power of two, S <= 64).
+// The value of lane ^ 32 (v_permlane32_swap, CDNA4): one VALU exchange
+// instead of a ds_bpermute round trip through the LDS crossbar.  Inline asm,
+// not the builtin: hipcc (ROCm 7.2) sinks the builtin into the branch of a
+// `cond ? v : half_swap(v)` select, where half the lanes are inactive and
+// the swap reads their unwritten registers (measured: wrong policy
+// gradients).  A volatile asm runs exactly where it is written, with every
+// lane active; `s_nop 1` is the 2 wait states a VALU write of either operand
+// needs before the swap reads it.
+__device__ __forceinline__ float half_swap(float v) {
+  unsigned a = __float_as_uint(v), b = a;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  // a: lanes 32-63 now hold lanes 0-31's value; b: lanes 0-31 hold 32-63's
+  return __uint_as_float((threadIdx.x & 32) ? a : b);
+}
+
+// v + (v of a partner lane) through a DPP lane pattern (a VALU modifier, no
+// LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(
+                 __builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned segments of S lanes (S a power of two, S <= 64).  The
+// result is bit-identical to the xor butterfly v += shfl_xor(v, o) for
+// o = 1, 2, .., S/2: every stage adds the partner's partial sum, and the DPP
+// patterns used (quad_perm [1,0,3,2] / [2,3,0,1] = xor 1 / 2, row_half_mirror
+// i <-> 7-i, row_mirror i <-> 15-i) pair each lane with a lane holding the
+// same partial sum as its xor-4 / xor-8 partner; float addition commutes, so
+// every lane of a segment ends with the same bits as the butterfly.  The last
+// two stages of a full wave read the four row sums with v_readlane.
 template <int S>
 __device__ __forceinline__ float seg_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < S; o <<= 1) v += __shfl_xor(v, o, kWave);
+  if constexpr (S >= 2) v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (S >= 4) v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (S >= 8) v = dpp_add<0x141>(v);  // row_half_mirror
+  if constexpr (S >= 16) v = dpp_add<0x140>(v); // row_mirror
+  if constexpr (S == 32) v += __shfl_xor(v, 16, kWave);
+  if constexpr (S == 64) {
+    const int b = __float_as_int(v);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(b, 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(b, 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(b, 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(b, 48));
+    v = (r0 + r1) + (r2 + r3);
+  }
   return v;
 }
 template <int S>
