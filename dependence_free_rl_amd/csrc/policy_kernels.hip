@@ -1231,12 +1231,15 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         const float zs = ((lds[S::L_Z + r] + lds[S::L_Z + R + r]) +
                           lds[S::L_Z + 2 * R + r]) + lds[S::L_Z + 3 * R + r];
         z[k] = zs + lds[S::L_B3];
-        ex[k] = expf(z[k]);
+        ex[k] = __expf(z[k]);
         se += ex[k];
       }
       se = seg_sum<SEG>(se);
+      // serial phase (no MFMA beside it): v_exp / v_rcp forms (<= 2 ulp)
+      // instead of the IEEE sequences, well inside the 1e-4 parity bound
+      const float rse = __builtin_amdgcn_rcpf(se);
 #pragma unroll
-      for (int k = 0; k < HG; ++k) p[k] = ex[k] / se;
+      for (int k = 0; k < HG; ++k) p[k] = ex[k] * rse;
       const int c = c_cur;
       const float A = A_cur;
       const int seg0 = (lane / SEG) * SEG;
@@ -1261,14 +1264,14 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         } else if (a.algo == kPPO) {
           // clipped_gradient (rl.h:54-74) + softmax_layer::backward
           // (nn.h:393-417): gz_j = (diag(p) - p p^T)[j][c] * g_c
-          const float ratio = pc / po_cur;
+          const float ratio = pc * __builtin_amdgcn_rcpf(po_cur);
           float clipped = ratio;
           if (ratio > 1.0f + a.clip_eps)
             clipped = 1.0f + a.clip_eps;
           else if (ratio < 1.0f - a.clip_eps)
             clipped = 1.0f - a.clip_eps;
           const float ig = fminf(clipped * A, ratio * A) * -1.0f;
-          const float gc = ig / pc;
+          const float gc = ig * __builtin_amdgcn_rcpf(pc);
           const float lin = bin == c ? p[k] : 0.0f;
           gz = (lin - p[k] * pc) * gc;
         } else {
