@@ -1315,7 +1315,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
 
       // ---- dH1 tile q of r-tile rt (K = H2)
       f32x16 dh = zero16();
-#pragma unroll 8
+#pragma unroll 16
       for (int s = 0; s < S::H2 / 2; ++s) {
         if (XH_DIAG_ABLATE && (a.ablate & 16)) break;
         const int k = 2 * s + h;
