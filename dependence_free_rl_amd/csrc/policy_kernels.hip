@@ -1105,6 +1105,13 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   // features are constant per env and take one of the two table values
   // (bin_packing.h:73-74), so their columns (and db1) are carried as the
   // dA1 sums over rows holding item_a (sA) and item_b (sB).
+  // kB2Late (128-row groups, the register-bound D=3 variant): db2 of H2 unit
+  // q*32 + lr is summed from the dA2 image rows the dW2 loop reads anyway
+  // (wave rt takes row quads 4rt..4rt+3 of its lane half): 15 registers
+  // fewer than accB2[16] (spills 344 -> 272 B per lane).  The 64-row kernel
+  // keeps the adds in the layer-3 phase (measured 0.1% faster there).
+  constexpr bool kB2Late = S::HG > 1;
+  float b2s = 0.0f;
   float accW1[16][S::D], sA[16], sB[16], accW3[16], accB2[16], accB3 = 0.0f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -1306,7 +1313,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
             const float v = pre[j];
             accW3[j] += gr * relu(v);
             const float d = v > 0.0f ? gr * wq[u] : 0.0f;
-            accB2[j] += d;
+            if (!kB2Late) accB2[j] += d;
             DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
           }
         }
@@ -1346,6 +1353,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         const float4 av = lds4(pa + 4 * s4);
         const float4 b0 = lds4(pb0 + 4 * s4);
         const float4 b1 = lds4(pb1 + 4 * s4);
+        if (kB2Late && (s4 >> 2) == rt) b2s += (av.x + av.y) + (av.z + av.w);
         accW2[0] = mfma32(av.x, b0.x, accW2[0]);
         accW2[1] = mfma32(av.x, b1.x, accW2[1]);
         accW2[0] = mfma32(av.y, b0.y, accW2[0]);
@@ -1418,8 +1426,12 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
             vb * ((float)a.env.item_b[d] / (float)kCapacity);
       my[S::H1 * S::F0 + i] = va + vb;
       my[S::H1 * S::F0 + S::H1 + i] = vw3;  // o2 = q*32 + acc_row too
-      my[S::H1 * S::F0 + S::H1 + S::H2 + i] = vb2;
+      if (!kB2Late) my[S::H1 * S::F0 + S::H1 + S::H2 + i] = vb2;
     }
+  }
+  if (kB2Late) {  // db2: lane halves hold the two 32-row halves of a unit
+    const float v = b2s + __shfl_xor(b2s, 32, kWave);
+    if (h == 0) my[S::H1 * S::F0 + S::H1 + S::H2 + q * 32 + lr] = v;
   }
   {
     float v = accB3;
