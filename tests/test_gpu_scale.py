@@ -188,3 +188,55 @@ def test_wave_rollout_matches_4wave(ctx, monkeypatch):
         else:  # ~0.03% of the logits differ in the last place
             np.testing.assert_allclose(x, y, rtol=2e-6, atol=1e-7,
                                        err_msg="buffer %d" % b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,N,B,D,T,items", [
+    ("ppo", 4096, 32, 1, 4, ([4], [1])),                    # BASELINE config 2
+    ("ac", 16384, 128, 3, 8, ([4, 2, 2], [1, 2, 1])),      # config 5 per GPU
+])
+def test_other_configs_full_size_properties(ctx, algo, N, B, D, T, items):
+    """BASELINE configs 2 and 5 at their per-GPU sizes: env transition
+    invariants on every env and step, probability normalisation, finite
+    learner state, and bitwise run-to-run determinism (as config 3 above)."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_ADV, BUF_BINS,
+                                                BUF_DONE, BUF_ITEMS, BUF_POLD)
+    H = (64, 64) if B == 32 else (128, 128)
+    pp, vp = init_policy(D, *H, seed=3), init_value(B, D, seed=4)
+
+    def make():
+        tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
+                     widths=H, rng_state=777)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        return tr
+
+    tr = make()
+    tr.iterate(1)
+    tr.rollout()
+    bins = tr.buffer(BUF_BINS).astype(np.int32).reshape(T + 1, N, B, D)
+    it = tr.buffer(BUF_ITEMS).reshape(T + 1, N, 4)[:, :, :D].astype(np.int32)
+    act = tr.buffer(BUF_ACTION).reshape(T, N)
+    done = tr.buffer(BUF_DONE).reshape(T, N)
+    assert bins.min() >= 0 and bins.max() <= 8
+    assert act.min() >= 0 and act.max() < B
+    ok = (it == items[0]).all(-1) | (it == items[1]).all(-1)
+    assert ok.all()
+    idx = np.arange(N)
+    for t in range(T):
+        nxt = bins[t].copy()
+        nxt[idx, act[t]] -= it[t]
+        over = (nxt[idx, act[t]] < 0).any(-1)
+        np.testing.assert_array_equal(over.astype(np.uint8), done[t])
+        np.testing.assert_array_equal(bins[t + 1][~over], nxt[~over])
+        assert (bins[t + 1][over] == 8).all()
+    pold = tr.buffer(BUF_POLD)
+    assert (pold > 0).all() and (pold <= 1).all()
+    tr.learn()
+    p1 = tr.params(POLICY)
+    assert np.isfinite(p1).all() and np.isfinite(tr.params(VALUE)).all()
+    assert np.isfinite(tr.buffer(BUF_ADV)).all()
+    tr2 = make()
+    tr2.iterate(2)
+    np.testing.assert_array_equal(tr2.params(POLICY), p1)
