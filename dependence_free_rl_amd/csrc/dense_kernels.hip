@@ -12,6 +12,8 @@
 //                                             over rows into per-split slabs
 // One dimension may be a device-side row count (rows of this learn() batch),
 // so a launch needs no host synchronisation.
+#include <type_traits>
+
 #include "xh_device.h"
 #include "xh_kernels.h"
 
@@ -28,12 +30,14 @@ struct RowMajor {  // p[i * ld + k]
   const float *p;
   int ld;
   static constexpr bool kKContig = true;
+  static constexpr bool kRowCtx = false;
   __device__ float operator()(int i, int k) const { return p[(size_t)i * ld + k]; }
 };
 struct ColMajor {  // p[k * ld + i]
   const float *p;
   int ld;
   static constexpr bool kKContig = false;
+  static constexpr bool kRowCtx = false;
   __device__ float operator()(int i, int k) const { return p[(size_t)k * ld + i]; }
 };
 // [X | 1] as the B operand of a weight gradient: element (n, k=row) =
@@ -42,6 +46,7 @@ struct RowsOnes {
   const float *p;
   int ld, ncol;
   static constexpr bool kKContig = false;
+  static constexpr bool kRowCtx = false;
   __device__ float operator()(int n, int r) const {
     return n < ncol ? p[(size_t)r * ld + n] : 1.0f;
   }
@@ -59,28 +64,41 @@ struct ObsRows {
   int N, slot;
   const int32_t *action;
   int term_from;
-  __device__ float feature(int r, int k) const {
-    const int D = E.D, bin = k / (2 * D), c = k - bin * 2 * D;
-    int idx, sub = -1;
+  // (slot*N + env, terminal action or -1) of row r: resolved once per row
+  struct RowCtx {
+    int idx, sub;
+  };
+  __device__ RowCtx ctx(int r) const {
+    RowCtx c{0, -1};
     if (action && r >= term_from) {
-      idx = r - term_from;
-      sub = action[idx];
+      c.idx = r - term_from;
+      c.sub = action[c.idx];
     } else {
-      idx = list ? list[r] : slot * N + r;
+      c.idx = list ? list[r] : slot * N + r;
     }
-    int v = c < D ? bins[(size_t)idx * E.B * D + bin * D + c]
-                  : items[(size_t)idx * 4 + c - D];
-    if (c < D && bin == sub) v -= items[(size_t)idx * 4 + c];
+    return c;
+  }
+  __device__ float feature_at(RowCtx rc, int k) const {
+    const int D = E.D, bin = k / (2 * D), c = k - bin * 2 * D;
+    int v = c < D ? bins[(size_t)rc.idx * E.B * D + bin * D + c]
+                  : items[(size_t)rc.idx * 4 + c - D];
+    if (c < D && bin == rc.sub) v -= items[(size_t)rc.idx * 4 + c];
     return (float)v * (1.0f / (float)kCapacity);
   }
+  __device__ float feature(int r, int k) const { return feature_at(ctx(r), k); }
 };
 struct ObsA : ObsRows {  // A operand: (m = row, k = feature)
   static constexpr bool kKContig = true;
+  // a thread's rows are fixed for the whole K loop: the GEMM resolves them
+  // once per tile (ctx) instead of once per K slice
+  static constexpr bool kRowCtx = true;
   __device__ float operator()(int r, int k) const { return feature(r, k); }
+  __device__ float at(RowCtx rc, int k) const { return feature_at(rc, k); }
 };
 struct ObsOnesB : ObsRows {  // B operand of dW1: (n = feature | 1, k = row)
   int ncol;
   static constexpr bool kKContig = false;
+  static constexpr bool kRowCtx = false;
   __device__ float operator()(int n, int r) const {
     return n < ncol ? feature(r, n) : 1.0f;
   }
@@ -119,6 +137,17 @@ struct EpSlab {  // weight-gradient slab: [A(out x in), b(out)] of one layer
 };
 
 // ---------------------------------------------------------------- GEMM ----
+namespace detail {
+template <class L, bool = L::kRowCtx>
+struct CtxOf {
+  using type = int;
+};
+template <class L>
+struct CtxOf<L, true> {
+  using type = typename L::RowCtx;
+};
+}  // namespace detail
+
 // dyn: 0 = static sizes, 1 = M is *rows, 2 = K is *rows (each <= the static
 // bound).  Split-K: blockIdx.z takes K range [z*kper, (z+1)*kper).
 template <class LA, class LB, class EP>
@@ -151,13 +180,31 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
     }
   };
   float ra[4], rb[4];
+  // row contexts of this thread's four A rows (kKContig: i does not depend
+  // on the K slice), for loaders that gather rows
+  struct NoCtx {};
+  using Ctx = std::conditional_t<LA::kRowCtx, typename detail::CtxOf<LA>::type, NoCtx>;
+  Ctx rc[4];
+  if constexpr (LA::kRowCtx) {
+    static_assert(LA::kKContig, "row contexts need fixed rows per thread");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int i, kk;
+      pos(true, j, i, kk);
+      const int m = bm + i;
+      rc[j] = la.ctx(m < M ? m : 0);
+    }
+  }
   auto fetch = [&](int kb) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       int i, kk;
       pos(LA::kKContig, j, i, kk);
       const int m = bm + i, k = kb + kk;
-      ra[j] = (m < M && k < k1) ? la(m, k) : 0.0f;
+      if constexpr (LA::kRowCtx)
+        ra[j] = (m < M && k < k1) ? la.at(rc[j], k) : 0.0f;
+      else
+        ra[j] = (m < M && k < k1) ? la(m, k) : 0.0f;
       pos(LB::kKContig, j, i, kk);
       const int n = bn + i;
       rb[j] = (n < N && kb + kk < k1) ? lb(n, kb + kk) : 0.0f;
