@@ -240,3 +240,30 @@ def test_other_configs_full_size_properties(ctx, algo, N, B, D, T, items):
     tr2 = make()
     tr2.iterate(2)
     np.testing.assert_array_equal(tr2.params(POLICY), p1)
+
+
+def test_bench_json_line(tmp_path):
+    """bench.py end to end at a small size: one JSON line with the driver's
+    keys, the roofline / HBM objects, and whole-job arithmetic."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(
+        [sys.executable, os.path.join(repo, "bench.py"), "--steps", "2",
+         "--warmup", "1", "--envs", "256", "--no-cpu-baseline"],
+        capture_output=True, text=True, timeout=110, check=True, cwd=repo)
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+              "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+              "dtype", "data", "config", "roofline", "hbm_roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["envs_per_gpu"] == 256
+    # value = env-steps / time: 256 envs x T=4 per step
+    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 256 * 4) < 1e-3 * 256 * 4 + 1
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and r["peak"] == 157.3
