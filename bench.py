@@ -149,24 +149,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    rdzv = None
     uid = None
     device = local
     if world > 1:
         # one node by the bench contract: RCCL's bootstrap stays on loopback
-        # (the container hostname may not resolve); device = LOCAL_RANK, or
-        # modulo the visible devices if the launcher narrowed them per rank
+        # (the container hostname may not resolve).  No torch in this process
+        # (its bundled HIP / RCCL would shadow /opt/rocm's under the same
+        # sonames): the unique id, the barriers and the max-time reduce go
+        # over a plain TCP star (dependence_free_rl_amd/rendezvous.py).
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        import torch
-        ndev = torch.cuda.device_count()  # does not initialise the GPU
-        if ndev > 0 and local >= ndev:
+        from dependence_free_rl_amd import Context, device_count
+        from dependence_free_rl_amd.rendezvous import Rendezvous
+        ndev = device_count()
+        if ndev > 0 and local >= ndev:  # launcher narrowed the visible devices
             device = local % ndev
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        from dependence_free_rl_amd import Context
-        obj = [Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+        rdzv = Rendezvous(rank, world)
+        uid = rdzv.broadcast(Context.unique_id() if rank == 0 else None)
 
     from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
                                         init_policy, init_value)
@@ -182,21 +181,18 @@ def main():
     if args.warmup:
         tr.iterate(args.warmup)
     tr.synchronize()
-    if dist:
-        dist.barrier()
+    if rdzv:
+        rdzv.barrier()
     tr.set_timing(True)
     tr.reset_timing()
     t0 = time.perf_counter()
     tr.iterate(args.steps)
     tr.synchronize()
-    if dist:
-        dist.barrier()
+    if rdzv:
+        rdzv.barrier()
     dt = time.perf_counter() - t0
-    if dist:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    if rdzv:
+        dt = rdzv.allreduce_max(dt)
 
     ms_pt, n_pt = tr.kernel_time("policy_train")
     ms_ro, n_ro = tr.kernel_time("rollout_step")
@@ -274,8 +270,8 @@ def main():
         print(json.dumps(line), flush=True)
     tr.close()
     ctx.close()
-    if dist:
-        dist.destroy_process_group()
+    if rdzv:
+        rdzv.close()
 
 
 if __name__ == "__main__":

@@ -61,6 +61,8 @@ def _load():
         "xh_last_error": (C.c_char_p, []),
         "xh_version": (C.c_char_p, []),
         "xh_struct_size": (sz, [C.c_char_p]),
+        "xh_device_count": (i, [C.POINTER(C.c_int)]),
+        "xh_runtime_info": (i, [C.c_char_p, sz]),
         "xh_comm_unique_id": (i, [vp]),
         "xh_ctx_create": (i, [i, i, i, vp, C.POINTER(vp)]),
         "xh_ctx_destroy": (i, [vp]),
@@ -110,6 +112,20 @@ def check(status):
         raise XhError("xylo-hip status %d: %s" % (
             status, lib.xh_last_error().decode(errors="replace")))
     return status
+
+
+def runtime_info():
+    """The HIP / RCCL shared objects this process bound (xh_runtime_info)."""
+    import json
+    buf = C.create_string_buffer(4096)
+    check(lib.xh_runtime_info(buf, len(buf)))
+    return json.loads(buf.value.decode())
+
+
+def device_count():
+    n = C.c_int()
+    check(lib.xh_device_count(C.byref(n)))
+    return n.value
 
 
 def header_symbols():

@@ -29,6 +29,15 @@
 #ifndef XH_DIAG_ABLATE
 #define XH_DIAG_ABLATE 0
 #endif
+// Every ablation test folds to `false` in the product build, so a stray
+// XH_ABLATE in the environment cannot change what the shipped kernels compute
+// (the host refuses it too: xylo_hip.cpp do_learn).
+#define XH_ABL(a, k) (XH_DIAG_ABLATE && ((a).ablate & (k)))
+
+namespace xh {
+// 1 in the diagnostic build (make diag), 0 in the product library.
+int diag_build() { return XH_DIAG_ABLATE; }
+}  // namespace xh
 
 namespace xh {
 
@@ -847,7 +856,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
           h1own[1] = h1[it][1];
         }
       if (fwd_active) {
-        if (!(a.ablate & 4)) {
+        if (!XH_ABL(a, 4)) {
           layer2<S, S::FJ>(lds, h1, o2t, rt0, pre);
         } else {
 #pragma unroll
@@ -884,7 +893,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
         gz = v_cur ? p * (gp - sg) : 0.0f;
         if (w == 0 && v_cur)
           kl_acc += (double)q_cur * log((double)q_cur / (double)p);
-      } else if (a.ablate & 8) {
+      } else if (XH_ABL(a, 8)) {
         gz = z * 1e-3f;
       } else if (a.algo == kPPO) {
         // clipped_gradient (rl.h:54-74) then softmax_layer::backward
@@ -936,7 +945,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
     // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows); the JW
     // independent accumulation chains share the dA2 operand
 #pragma unroll 4
-    for (int s = 0; s < ((a.ablate & 1) ? 0 : 32); ++s) {
+    for (int s = 0; s < (XH_ABL(a, 1) ? 0 : 32); ++s) {
       const int r = 2 * s + h;
       const float av = DAimg[r * S::AS + o2t * 32 + lr];
 #pragma unroll
@@ -953,7 +962,7 @@ __global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a)
 #pragma unroll
       for (int q = 0; q < S::JH; ++q) dh[q] = zero16();
 #pragma unroll 4
-      for (int s = 0; s < ((a.ablate & 2) ? 0 : S::H2 / 2); ++s) {
+      for (int s = 0; s < (XH_ABL(a, 2) ? 0 : S::H2 / 2); ++s) {
         const int k = 2 * s + h;
         const float av = lds[S::L_W2 + k * S::W2S + it_own * 32 + lr];
 #pragma unroll
@@ -1186,7 +1195,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         for (int j = 0; j < 16; ++j)
           H1T[(it * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = t1[j];
       }
-      if (a.ablate & 4) continue;
+      if (XH_ABL(a, 4)) continue;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const float4 a4 = lds4(wrow + it * 32 + 8 * qq);
@@ -1266,7 +1275,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       for (int k = 0; k < HG; ++k) {
         const int bin = (k * 64 + lane) % B;
         float gz;
-        if (a.ablate & 8) {
+        if (XH_ABL(a, 8)) {
           gz = z[k] * 1e-3f;
         } else if (a.algo == kPPO) {
           // clipped_gradient (rl.h:54-74) + softmax_layer::backward
@@ -1324,7 +1333,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       f32x16 dh = zero16();
 #pragma unroll 16
       for (int s = 0; s < S::H2 / 2; ++s) {
-        if (XH_DIAG_ABLATE && (a.ablate & 16)) break;
+        if (XH_ABL(a, 16)) break;
         const int k = 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
                     DAT[k * S::TS + rt * 32 + lr], dh);
@@ -1349,7 +1358,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
 #pragma unroll
       for (int s4 = 0; s4 < 8; ++s4) {
-        if (XH_DIAG_ABLATE && (a.ablate & 32)) break;
+        if (XH_ABL(a, 32)) break;
         const float4 av = lds4(pa + 4 * s4);
         const float4 b0 = lds4(pb0 + 4 * s4);
         const float4 b1 = lds4(pb1 + 4 * s4);

@@ -79,8 +79,9 @@ struct PolicyTrainArgs {
   const float *adv;  // [T][N]
   float *slab;       // [gridDim.x][slab_stride]
   int slab_stride;
-  int ablate;        // diagnostics only (XH_ABLATE): bit0 skip dW2, bit1 skip
-                     // dH1/dW1, bit2 skip layer-2 fwd, bit3 skip softmax/loss
+  int ablate;        // diagnostic build only (XH_ABLATE, make diag): bit0 skip
+                     // dW2, bit1 skip dH1/dW1, bit2 skip layer-2 fwd, bit3
+                     // skip softmax/loss; folded away in the product build
   // KL-PPO (kl_regulated_loss): every row of the learner's state matrix,
   // i.e. the T*N transitions, the open trajectories' end rows (slot T) and
   // the terminal end rows E_t listed in end_list.
@@ -208,6 +209,10 @@ hipError_t launch_pg_step(const PgStepArgs &a, hipStream_t s);
 hipError_t launch_pg_rows(const PgLearnArgs &a, hipStream_t s);
 hipError_t launch_pg_adv(const PgLearnArgs &a, hipStream_t s);
 hipError_t launch_pg_loss(const PgLearnArgs &a, int max_rows, hipStream_t s);
+
+// 1 when the kernels were built with the phase-ablation switches
+// (make diag, -DXH_DIAG_ABLATE=1), 0 in the product library.
+int diag_build();
 
 bool heuristic_shape_supported(int B, int D);
 hipError_t launch_heuristic(const HeuristicArgs &a, int kind, hipStream_t s);

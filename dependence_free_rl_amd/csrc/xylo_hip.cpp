@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -368,15 +370,18 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
     st = copy_ok(hipMemcpyAsync(scratch + o_init, e->init_items,
                                 4 * (size_t)n * D, hipMemcpyHostToDevice, s));
   }
+  // from here on a failure is recorded in `st` and the scratch block, the
+  // events and the stream are still released / drained below
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  if (st == XH_OK) {
-    HIPCHK(hipEventCreate(&ev0));
-    HIPCHK(hipEventCreate(&ev1));
-    HIPCHK(hipEventRecord(ev0, s));
-    const hipError_t le = launch(eb);
-    if (le != hipSuccess)
-      st = fail(XH_ERR_HIP, "evaluate launch: %s", hipGetErrorString(le));
-    HIPCHK(hipEventRecord(ev1, s));
+  auto hip_ok = [&](hipError_t e, const char *what) {
+    if (st == XH_OK && e != hipSuccess)
+      st = fail(XH_ERR_HIP, "evaluate %s: %s", what, hipGetErrorString(e));
+    return st == XH_OK;
+  };
+  if (st == XH_OK && hip_ok(hipEventCreate(&ev0), "event") &&
+      hip_ok(hipEventCreate(&ev1), "event") &&
+      hip_ok(hipEventRecord(ev0, s), "event record")) {
+    if (hip_ok(launch(eb), "launch")) hip_ok(hipEventRecord(ev1, s), "event record");
   }
   auto out = [&](void *host, size_t off, size_t nb) {
     if (st == XH_OK && host)
@@ -389,14 +394,12 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
   out(e->final_items, o_fin, 4 * (size_t)n * D);
   out(e->trace, o_trace, 4 * (size_t)eb.trace_cap);
   (void)hipFreeAsync(scratch, s);
-  HIPCHK(hipStreamSynchronize(s));
-  if (ev0 && ev1) {
-    float ms = 0.0f;
-    if (st == XH_OK && hipEventElapsedTime(&ms, ev0, ev1) == hipSuccess)
-      e->elapsed_ms = ms;
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
-  }
+  hip_ok(hipStreamSynchronize(s), "synchronize");
+  float ms = 0.0f;
+  if (st == XH_OK && hipEventElapsedTime(&ms, ev0, ev1) == hipSuccess)
+    e->elapsed_ms = ms;
+  if (ev0) (void)hipEventDestroy(ev0);
+  if (ev1) (void)hipEventDestroy(ev1);
   return st;
 }
 
@@ -527,8 +530,14 @@ int do_learn(xh_trainer *t) {
   pa.slab = t->pslab;
   pa.slab_stride = t->pslab_stride;
   {
-    const char *ab = std::getenv("XH_ABLATE");  // diagnostics only
+    // XH_ABLATE drops whole phases (wrong results by design): honoured by the
+    // diagnostic build only, refused by the product library
+    const char *ab = std::getenv("XH_ABLATE");
     pa.ablate = ab ? std::atoi(ab) : 0;
+    if (pa.ablate && !xh::diag_build())
+      return fail(XH_ERR_INVALID, "XH_ABLATE=%s is set but this is the "
+                  "product library (phase ablation exists only in `make "
+                  "diag`)", ab);
   }
   const bool kl = c.algo == XH_KLPPO;
   if (kl) {
@@ -800,7 +809,40 @@ int do_pg_learn(xh_trainer *t) {
 extern "C" {
 
 const char *xh_last_error(void) { return g_err.c_str(); }
-const char *xh_version(void) { return "xylo-hip 0.1 (gfx950)"; }
+const char *xh_version(void) { return "xylo-hip 0.2 (gfx950)"; }
+
+int xh_device_count(int *out) {
+  return guard([&]() -> int {
+    if (!out) return fail(XH_ERR_INVALID, "null out");
+    *out = 0;
+    HIPCHK(hipGetDeviceCount(out));
+    return XH_OK;
+  });
+}
+
+// Which HIP / RCCL shared objects this process actually bound (a process that
+// loaded another copy under the same soname first, e.g. a framework's bundled
+// runtime, makes the library bind that one).
+int xh_runtime_info(char *buf, size_t cap) {
+  return guard([&]() -> int {
+    if (!buf || cap == 0) return fail(XH_ERR_INVALID, "null buffer");
+    Dl_info hi{}, ri{};
+    const char *hp = dladdr(reinterpret_cast<void *>(&hipRuntimeGetVersion), &hi) &&
+                             hi.dli_fname ? hi.dli_fname : "?";
+    const char *rp = dladdr(reinterpret_cast<void *>(&ncclAllReduce), &ri) &&
+                             ri.dli_fname ? ri.dli_fname : "?";
+    int hv = 0, rv = 0;
+    (void)hipRuntimeGetVersion(&hv);
+    (void)ncclGetVersion(&rv);
+    const int n = std::snprintf(buf, cap,
+                                "{\"libamdhip64\": \"%s\", \"hip_runtime\": %d, "
+                                "\"librccl\": \"%s\", \"rccl_version\": %d}",
+                                hp, hv, rp, rv);
+    if (n < 0 || (size_t)n >= cap)
+      return fail(XH_ERR_INVALID, "runtime info needs %d bytes", n + 1);
+    return XH_OK;
+  });
+}
 
 size_t xh_struct_size(const char *name) {
   if (!name) return 0;
@@ -890,14 +932,23 @@ int xh_ctx_allreduce_host(xh_ctx *c, float *data, size_t n) {
     if (!c->comm || n == 0) return XH_OK;
     float *d = nullptr;
     HIPCHK(hipMalloc(&d, n * sizeof(float)));
-    HIPCHK(hipMemcpyAsync(d, data, n * sizeof(float), hipMemcpyHostToDevice,
-                          c->stream));
-    RCCLCHK(ncclAllReduce(d, d, n, ncclFloat32, ncclSum, c->comm, c->stream));
-    HIPCHK(hipMemcpyAsync(data, d, n * sizeof(float), hipMemcpyDeviceToHost,
-                          c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipFree(d));
-    return XH_OK;
+    // the device buffer is freed on every path (the stream drained first)
+    int st = copy_ok(hipMemcpyAsync(d, data, n * sizeof(float),
+                                    hipMemcpyHostToDevice, c->stream));
+    if (st == XH_OK) {
+      const ncclResult_t r =
+          ncclAllReduce(d, d, n, ncclFloat32, ncclSum, c->comm, c->stream);
+      if (r != ncclSuccess)
+        st = fail(XH_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    }
+    if (st == XH_OK)
+      st = copy_ok(hipMemcpyAsync(data, d, n * sizeof(float),
+                                  hipMemcpyDeviceToHost, c->stream));
+    const hipError_t se = hipStreamSynchronize(c->stream);
+    if (st == XH_OK && se != hipSuccess)
+      st = fail(XH_ERR_HIP, "synchronize: %s", hipGetErrorString(se));
+    (void)hipFree(d);
+    return st;
   });
 }
 

@@ -42,6 +42,12 @@ enum {
 const char *xh_last_error(void);
 /* Library version string. */
 const char *xh_version(void);
+/* Number of visible HIP devices (initialises the HIP runtime). */
+int xh_device_count(int *out);
+/* JSON object naming the HIP and RCCL shared objects this process bound and
+ * their versions: {"libamdhip64": path, "hip_runtime": n, "librccl": path,
+ * "rccl_version": n}.  Written NUL-terminated into buf[cap]. */
+int xh_runtime_info(char *buf, size_t cap);
 
 /* ------------------------------------------------------------ context --- */
 typedef struct xh_ctx xh_ctx;

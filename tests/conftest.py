@@ -64,3 +64,19 @@ def assert_params_close(x, y, mask=None, slack=0.0, what=""):
         what, "noise-level entries beyond 2*lr*steps",
         float(np.abs(x[mask] - y[mask]).max()), slack)
     return assert_close(x[~mask], y[~mask], what=what)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    """One device context per test module.  No torch in the process: torch
+    bundles its own libamdhip64 / librccl under the same sonames, and a
+    process that loaded them first would make libxylo_hip bind those instead
+    of /opt/rocm's (the runtime the bench measures on)."""
+    from dependence_free_rl_amd import Context, runtime_info
+    assert "torch" not in sys.modules, "GPU tests must not import torch"
+    info = runtime_info()
+    for key in ("libamdhip64", "librccl"):
+        assert "/torch/" not in info[key], info
+    c = Context(device=0)
+    yield c
+    c.close()

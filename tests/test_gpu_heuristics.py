@@ -12,14 +12,6 @@ pytestmark = pytest.mark.gpu
 KINDS = ["firstfit", "bestfit", "minwaste", "random"]
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 @pytest.mark.parametrize("kind", KINDS)
 def test_heuristic_matches_reference_agent(ctx, kind):

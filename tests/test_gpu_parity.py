@@ -16,14 +16,6 @@ from gpu_helpers import meta, row_index, step_major, trainer_from_golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401  (device discovery only; no torch compute)
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3",
              "klppo_b8d2"]

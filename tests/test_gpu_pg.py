@@ -15,14 +15,6 @@ from gpu_helpers import meta
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401  (device discovery only; no torch compute)
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 def pg_trainer(ctx, B, D, N, E, widths, x0, params):
     from dependence_free_rl_amd import POLICY, Trainer

@@ -14,14 +14,6 @@ from conftest import assert_params_close, noise_mask
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 def _trainer(ctx, pp, vp):
     from dependence_free_rl_amd import POLICY, VALUE, Trainer

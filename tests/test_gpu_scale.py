@@ -8,14 +8,6 @@ from conftest import assert_close
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     from oracle import pyoracle as po

@@ -18,14 +18,6 @@ from conftest import assert_close
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import torch  # noqa: F401
-    from dependence_free_rl_amd import Context
-    c = Context(device=0)
-    yield c
-    c.close()
-
 
 @pytest.mark.parametrize("n", [64, 16384])
 def test_two_shards_sum_to_full_batch(ctx, n):
