@@ -12,7 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall \
 OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
-            $(SRC)/pg_kernels.o $(SRC)/xylo_hip.o
+            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/xylo_hip.o
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified

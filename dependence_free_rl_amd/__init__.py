@@ -7,7 +7,8 @@ from .trainer import (ALGOS, POLICY, VALUE, Context, Trainer,  # noqa: F401
                       heuristic_evaluate, init_full_policy, init_policy,
                       init_value,
                       policy_param_count, value_param_count)
+from .venv import VecEnv  # noqa: F401
 
 __all__ = ["Context", "Trainer", "POLICY", "VALUE", "init_policy", "init_value",
            "init_full_policy",
-           "heuristic_evaluate", "XhError", "runtime_info", "device_count"]
+           "heuristic_evaluate", "XhError", "runtime_info", "device_count", "VecEnv"]

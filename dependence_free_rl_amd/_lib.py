@@ -17,6 +17,8 @@ XH_PPO, XH_AC, XH_KLPPO, XH_PG = 0, 1, 2, 3
 HEURISTICS = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
 XH_POLICY, XH_VALUE = 0, 1
 OPTIMIZERS = {"sgd": 0, "momentum": 1, "adam": 2}
+(VENV_ACTIONS, VENV_REWARD, VENV_DONE, VENV_BINS, VENV_ITEMS, VENV_RNG,
+ VENV_OBS, VENV_MASK) = range(8)
 (BUF_BINS, BUF_ITEMS, BUF_ACTION, BUF_POLD, BUF_DONE, BUF_RNG, BUF_V_STATE,
  BUF_V_TERM, BUF_TARGETS, BUF_ADV, BUF_VALUE_GRAD, BUF_POLICY_GRADS,
  BUF_LOGITS, BUF_PROBS, BUF_V_STATE0, BUF_QOLD, BUF_KL, BUF_LEN) = range(18)
@@ -91,6 +93,20 @@ def _load():
         "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_long)]),
         "xh_trainer_reset_timing": (i, [vp]),
+        "xh_trainer_get_env_state": (i, [vp, i, i, vp, vp]),
+        "xh_trainer_set_env_state": (i, [vp, i, i, vp, vp]),
+        "xh_venv_create": (i, [vp, i, i, i, C.c_uint32, i, i, i,
+                               C.POINTER(vp)]),
+        "xh_venv_destroy": (i, [vp]),
+        "xh_venv_bytes": (sz, [vp, i]),
+        "xh_venv_device_ptr": (vp, [vp, i]),
+        "xh_venv_get": (i, [vp, i, vp, sz]),
+        "xh_venv_set": (i, [vp, i, vp, sz]),
+        "xh_venv_step": (i, [vp, i]),
+        "xh_venv_apply": (i, [vp, i]),
+        "xh_venv_reset": (i, [vp, i]),
+        "xh_venv_observe": (i, [vp]),
+        "xh_venv_synchronize": (i, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -210,6 +210,29 @@ hipError_t launch_pg_rows(const PgLearnArgs &a, hipStream_t s);
 hipError_t launch_pg_adv(const PgLearnArgs &a, hipStream_t s);
 hipError_t launch_pg_loss(const PgLearnArgs &a, int max_rows, hipStream_t s);
 
+// Vectorised environment for callers with their own policy (xh_venv_*,
+// venv_kernels.hip): bins int8 [N][B*D], items int8 [N][4], rng u32 [N].
+enum VenvOp { kVenvStep = 0, kVenvReset = 1, kVenvObserve = 2 };
+struct VenvArgs {
+  EnvDesc env;
+  int N;
+  int8_t *bins, *items;
+  uint32_t *rng;
+  const int32_t *action;  // [N] chosen bins
+  const uint8_t *mask;    // [N] or nullptr (all envs)
+  float *reward;          // [N] (step)
+  uint8_t *done;          // [N] game_over after the apply
+  float *obs;             // [N][B][2D] or nullptr
+  int *err;               // device flag: an action was out of range
+  int mode;               // 0 environment::apply, 1 agent::step minus react
+  uint32_t skip_mul;      // a^policy_draws (step)
+  uint32_t jump_mul;      // a^(k (Nglobal - 1)) after a step (reference order)
+};
+bool venv_shape_supported(int B, int D);
+hipError_t launch_venv(const VenvArgs &a, int op, hipStream_t s);
+hipError_t launch_venv_init(const VenvArgs &a, uint32_t x0, int env_offset,
+                            int n_global, int k, hipStream_t s);
+
 // 1 when the kernels were built with the phase-ablation switches
 // (make diag, -DXH_DIAG_ABLATE=1), 0 in the product library.
 int diag_build();

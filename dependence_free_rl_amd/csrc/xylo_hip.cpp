@@ -160,6 +160,9 @@ struct xh_trainer {
   uint32_t jump_mul = 1;
   int rgrid = 0;
   bool need_shift = false;
+  // xh_trainer_set_env_state: states the next rollout starts from, keyed by
+  // env (B*D bin bytes then D item bytes), applied after the forget() shift
+  std::map<int, std::vector<int8_t>> env_override;
   bool use_forced = false;
   bool timing = false;
   bool counted = false;  // holds a reference on ctx
@@ -190,6 +193,34 @@ struct xh_trainer {
   size_t N() const { return (size_t)cfg.num_envs; }
   size_t T() const { return (size_t)Tb; }
   size_t BD() const { return (size_t)cfg.bins * cfg.dims; }
+};
+
+// N vectorised envs for a caller's own policy (xh_venv_*, venv_kernels.hip).
+struct xh_venv {
+  xh_ctx *ctx = nullptr;
+  xh::EnvDesc env{};
+  int N = 0, Ng = 0, offset = 0, policy_draws = 0;
+  uint32_t skip_mul = 1, jump_mul = 1;
+  void *buf[XH_VENV_BUF_COUNT] = {};
+  size_t bytes[XH_VENV_BUF_COUNT] = {};
+  int *err = nullptr;
+  bool counted = false;
+
+  xh::VenvArgs args() const {
+    xh::VenvArgs a{};
+    a.env = env;
+    a.N = N;
+    a.bins = (int8_t *)buf[XH_VENV_BINS];
+    a.items = (int8_t *)buf[XH_VENV_ITEMS];
+    a.rng = (uint32_t *)buf[XH_VENV_RNG];
+    a.action = (const int32_t *)buf[XH_VENV_ACTIONS];
+    a.reward = (float *)buf[XH_VENV_REWARD];
+    a.done = (uint8_t *)buf[XH_VENV_DONE];
+    a.err = err;
+    a.skip_mul = skip_mul;
+    a.jump_mul = jump_mul;
+    return a;
+  }
 };
 
 namespace {
@@ -300,6 +331,7 @@ int copy_ok(hipError_t e) {
 }
 
 constexpr uint64_t kEvalStride = 1ull << 26;  // draws between env streams
+constexpr int kBinCapacity = 8;             // bin_packing.h:48, every dim
 
 xh::EnvDesc make_env(int bins, int dims) {
   static const int ia[3][3] = {{4, 0, 0}, {4, 2, 0}, {4, 2, 2}};
@@ -426,6 +458,26 @@ int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
 int do_pg_rollout(xh_trainer *t);
 int do_pg_learn(xh_trainer *t);
 
+// Pending xh_trainer_set_env_state writes -> slot 0 (the rollout's S_0).  The
+// host vectors stay alive until the stream has consumed them (synchronised
+// before the map is cleared).
+int apply_env_overrides(xh_trainer *t) {
+  if (t->env_override.empty()) return XH_OK;
+  hipStream_t s = t->ctx->stream;
+  const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
+  for (auto &kv : t->env_override) {
+    const size_t e = (size_t)kv.first;
+    HIPCHK(hipMemcpyAsync(t->bins + e * BD, kv.second.data(), BD,
+                          hipMemcpyHostToDevice, s));
+    int8_t it[4] = {0, 0, 0, 0};
+    for (size_t d = 0; d < D; ++d) it[d] = kv.second[BD + d];
+    HIPCHK(hipMemcpyAsync(t->items + e * 4, it, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // `it` is a stack buffer
+  }
+  t->env_override.clear();
+  return XH_OK;
+}
+
 int do_rollout(xh_trainer *t) {
   if (t->cfg.algo == XH_PG) return do_pg_rollout(t);
   hipStream_t s = t->ctx->stream;
@@ -437,6 +489,7 @@ int do_rollout(xh_trainer *t) {
                           hipMemcpyDeviceToDevice, s));
     t->need_shift = false;
   }
+  CHK(apply_env_overrides(t));
   xh::RolloutArgs a{};
   a.env = t->env;
   a.b = t->batch();
@@ -1422,6 +1475,254 @@ int xh_trainer_kernel_time(xh_trainer *t, const char *name, double *ms,
     *ms = total;
     *launches = n;
     return XH_OK;
+  });
+}
+
+int xh_trainer_get_env_state(xh_trainer *t, int first, int count, int8_t *bins,
+                             int8_t *items) {
+  return guard([&]() -> int {
+    if (!t || (count && (!bins || !items)))
+      return fail(XH_ERR_INVALID, "null arg");
+    if (t->cfg.algo == XH_PG)
+      return fail(XH_ERR_INVALID, "env state access: not for XH_PG trainers");
+    if (first < 0 || count < 0 || first + count > t->cfg.num_envs)
+      return fail(XH_ERR_INVALID, "envs [%d, %d) of %d", first, first + count,
+                  t->cfg.num_envs);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    hipStream_t s = t->ctx->stream;
+    const size_t BD = t->BD(), D = (size_t)t->cfg.dims, N = t->N();
+    const size_t slot = t->need_shift ? t->T() : 0;
+    std::vector<int8_t> it((size_t)count * 4);
+    HIPCHK(hipMemcpyAsync(bins, t->bins + (slot * N + first) * BD,
+                          (size_t)count * BD, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(it.data(), t->items + (slot * N + first) * 4,
+                          (size_t)count * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int e = 0; e < count; ++e) {
+      auto o = t->env_override.find(first + e);
+      if (o != t->env_override.end()) {
+        std::memcpy(bins + (size_t)e * BD, o->second.data(), BD);
+        std::memcpy(items + (size_t)e * D, o->second.data() + BD, D);
+      } else {
+        std::memcpy(items + (size_t)e * D, it.data() + (size_t)e * 4, D);
+      }
+    }
+    return XH_OK;
+  });
+}
+
+int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
+                             const int8_t *bins, const int8_t *items) {
+  return guard([&]() -> int {
+    if (!t || (count && (!bins || !items)))
+      return fail(XH_ERR_INVALID, "null arg");
+    if (t->cfg.algo == XH_PG)
+      return fail(XH_ERR_INVALID, "env state access: not for XH_PG trainers");
+    if (first < 0 || count < 0 || first + count > t->cfg.num_envs)
+      return fail(XH_ERR_INVALID, "envs [%d, %d) of %d", first, first + count,
+                  t->cfg.num_envs);
+    const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
+    for (size_t i = 0; i < (size_t)count * BD; ++i)
+      if (bins[i] > kBinCapacity)
+        return fail(XH_ERR_INVALID, "bin value %d above capacity", bins[i]);
+    for (size_t i = 0; i < (size_t)count * D; ++i)
+      if (items[i] != t->env.item_a[i % D] && items[i] != t->env.item_b[i % D])
+        return fail(XH_ERR_INVALID, "item value %d is not in the item table",
+                    items[i]);
+    for (int e = 0; e < count; ++e) {
+      std::vector<int8_t> v(BD + D);
+      std::memcpy(v.data(), bins + (size_t)e * BD, BD);
+      std::memcpy(v.data() + BD, items + (size_t)e * D, D);
+      t->env_override[first + e] = std::move(v);
+    }
+    return XH_OK;
+  });
+}
+
+// ------------------------------------------------------------------ venv --
+int xh_venv_create(xh_ctx *ctx, int num_envs, int bins, int dims,
+                   uint32_t rng_state, int env_offset, int num_envs_global,
+                   int policy_draws, xh_venv **out) {
+  return guard([&]() -> int {
+    if (!ctx || !out) return fail(XH_ERR_INVALID, "null arg");
+    if (!xh::venv_shape_supported(bins, dims))
+      return fail(XH_ERR_INVALID, "venv: bins %d (8/16/32/64/128), dims %d "
+                  "(1..3)", bins, dims);
+    if (num_envs < 1 || env_offset < 0 || num_envs_global < num_envs ||
+        env_offset + num_envs > num_envs_global)
+      return fail(XH_ERR_INVALID, "venv: envs %d at offset %d of %d", num_envs,
+                  env_offset, num_envs_global);
+    if (policy_draws < 0 || policy_draws > 64)
+      return fail(XH_ERR_INVALID, "venv: policy_draws %d", policy_draws);
+    HIPCHK(hipSetDevice(ctx->device));
+    auto *v = new xh_venv;
+    v->ctx = ctx;
+    v->env = make_env(bins, dims);
+    v->N = num_envs;
+    v->Ng = num_envs_global;
+    v->offset = env_offset;
+    v->policy_draws = policy_draws;
+    const uint64_t k = (uint64_t)policy_draws + 2;
+    v->skip_mul = mstd_pow((uint64_t)policy_draws);
+    v->jump_mul = mstd_pow(k * (uint64_t)(num_envs_global - 1));
+    const size_t N = (size_t)num_envs, BD = (size_t)bins * dims;
+    const size_t sz[XH_VENV_BUF_COUNT] = {N * 4, N * 4, N, N * BD, N * 4, N * 4,
+                                          N * BD * 2 * 4, N};
+    int st = XH_OK;
+    for (int b = 0; b < XH_VENV_BUF_COUNT && st == XH_OK; ++b) {
+      v->bytes[b] = sz[b];
+      if (hipMalloc(&v->buf[b], sz[b]) != hipSuccess ||
+          hipMemset(v->buf[b], 0, sz[b]) != hipSuccess)
+        st = fail(XH_ERR_HIP, "venv: allocating %zu bytes", sz[b]);
+    }
+    if (st == XH_OK && (hipMalloc((void **)&v->err, 4) != hipSuccess ||
+                        hipMemset(v->err, 0, 4) != hipSuccess))
+      st = fail(XH_ERR_HIP, "venv: error flag");
+    if (st == XH_OK) {
+      uint32_t x0 = rng_state % 2147483647u;
+      const hipError_t e = xh::launch_venv_init(v->args(), x0 ? x0 : 1u,
+                                                env_offset, num_envs_global,
+                                                (int)k, ctx->stream);
+      if (e != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
+        st = fail(XH_ERR_HIP, "venv init: %s", hipGetErrorString(e));
+    }
+    v->counted = true;
+    ++ctx->trainers;
+    if (st != XH_OK) {
+      std::string keep = g_err;
+      xh_venv_destroy(v);
+      g_err = keep;
+      return st;
+    }
+    *out = v;
+    return XH_OK;
+  });
+}
+
+int xh_venv_destroy(xh_venv *v) {
+  return guard([&]() -> int {
+    if (!v) return XH_OK;
+    (void)hipSetDevice(v->ctx->device);
+    (void)hipStreamSynchronize(v->ctx->stream);
+    for (void *p : v->buf)
+      if (p) (void)hipFree(p);
+    if (v->err) (void)hipFree(v->err);
+    xh_ctx *c = v->ctx;
+    const bool counted = v->counted;
+    delete v;
+    if (counted && --c->trainers == 0 && c->closing) ctx_free(c);
+    return XH_OK;
+  });
+}
+
+size_t xh_venv_bytes(const xh_venv *v, int which) {
+  return v && which >= 0 && which < XH_VENV_BUF_COUNT ? v->bytes[which] : 0;
+}
+
+void *xh_venv_device_ptr(xh_venv *v, int which) {
+  return v && which >= 0 && which < XH_VENV_BUF_COUNT ? v->buf[which] : nullptr;
+}
+
+namespace {
+int venv_check_err(xh_venv *v) {
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, v->err, 4, hipMemcpyDeviceToHost, v->ctx->stream));
+  HIPCHK(hipStreamSynchronize(v->ctx->stream));
+  if (err) {
+    HIPCHK(hipMemset(v->err, 0, 4));
+    return fail(XH_ERR_INVALID, "venv: an action was outside [0, %d); those "
+                "envs were left untouched", v->env.B);
+  }
+  return XH_OK;
+}
+int venv_launch(xh_venv *v, int op, int mode, bool use_mask, bool obs) {
+  HIPCHK(hipSetDevice(v->ctx->device));
+  xh::VenvArgs a = v->args();
+  a.mode = mode;
+  a.mask = use_mask ? (const uint8_t *)v->buf[XH_VENV_MASK] : nullptr;
+  a.obs = obs ? (float *)v->buf[XH_VENV_OBS] : nullptr;
+  if (op == xh::kVenvObserve) a.obs = (float *)v->buf[XH_VENV_OBS];
+  if (mode == 0) a.reward = nullptr;
+  const hipError_t e = xh::launch_venv(a, op, v->ctx->stream);
+  if (e != hipSuccess)
+    return fail(XH_ERR_HIP, "venv launch: %s", hipGetErrorString(e));
+  return XH_OK;
+}
+}  // namespace
+
+int xh_venv_get(xh_venv *v, int which, void *host, size_t bytes) {
+  return guard([&]() -> int {
+    if (!v || !host) return fail(XH_ERR_INVALID, "null arg");
+    if (which < 0 || which >= XH_VENV_BUF_COUNT || bytes != v->bytes[which])
+      return fail(XH_ERR_INVALID, "venv buffer %d: %zu bytes, expected %zu",
+                  which, bytes, xh_venv_bytes(v, which));
+    HIPCHK(hipSetDevice(v->ctx->device));
+    HIPCHK(hipMemcpyAsync(host, v->buf[which], bytes, hipMemcpyDeviceToHost,
+                          v->ctx->stream));
+    return venv_check_err(v);
+  });
+}
+
+int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes) {
+  return guard([&]() -> int {
+    if (!v || !host) return fail(XH_ERR_INVALID, "null arg");
+    if (which < 0 || which >= XH_VENV_BUF_COUNT || bytes != v->bytes[which])
+      return fail(XH_ERR_INVALID, "venv buffer %d: %zu bytes, expected %zu",
+                  which, bytes, xh_venv_bytes(v, which));
+    if (which == XH_VENV_ACTIONS) {
+      const int32_t *a = static_cast<const int32_t *>(host);
+      for (int i = 0; i < v->N; ++i)
+        if (a[i] < 0 || a[i] >= v->env.B)
+          return fail(XH_ERR_INVALID, "venv: action %d of env %d outside "
+                      "[0, %d)", a[i], i, v->env.B);
+    }
+    if (which == XH_VENV_BINS) {
+      const int8_t *b = static_cast<const int8_t *>(host);
+      for (size_t i = 0; i < bytes; ++i)
+        if (b[i] > kBinCapacity)
+          return fail(XH_ERR_INVALID, "venv: bin value %d above capacity", b[i]);
+    }
+    HIPCHK(hipSetDevice(v->ctx->device));
+    HIPCHK(hipMemcpyAsync(v->buf[which], host, bytes, hipMemcpyHostToDevice,
+                          v->ctx->stream));
+    HIPCHK(hipStreamSynchronize(v->ctx->stream));
+    return XH_OK;
+  });
+}
+
+int xh_venv_step(xh_venv *v, int write_obs) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    return venv_launch(v, xh::kVenvStep, 1, false, write_obs != 0);
+  });
+}
+
+int xh_venv_apply(xh_venv *v, int use_mask) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    return venv_launch(v, xh::kVenvStep, 0, use_mask != 0, false);
+  });
+}
+
+int xh_venv_reset(xh_venv *v, int use_mask) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    return venv_launch(v, xh::kVenvReset, 0, use_mask != 0, false);
+  });
+}
+
+int xh_venv_observe(xh_venv *v) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    return venv_launch(v, xh::kVenvObserve, 0, false, true);
+  });
+}
+
+int xh_venv_synchronize(xh_venv *v) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    HIPCHK(hipSetDevice(v->ctx->device));
+    return venv_check_err(v);
   });
 }
 

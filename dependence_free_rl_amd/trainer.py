@@ -283,6 +283,27 @@ class Trainer:
         a = np.ascontiguousarray(arr, dt).reshape(shape)
         check(_lib.lib.xh_trainer_set_buffer(self.h, which, _ptr(a), a.nbytes))
 
+    def env_state(self, first=0, count=None):
+        """(bins [count][B][D], items [count][D]) int8: the states the next
+        rollout starts from (xh_trainer_get_env_state)."""
+        count = self.N - first if count is None else count
+        bins = np.zeros((count, self.B, self.D), np.int8)
+        items = np.zeros((count, self.D), np.int8)
+        check(_lib.lib.xh_trainer_get_env_state(self.h, first, count,
+                                                _ptr(bins), _ptr(items)))
+        return bins, items
+
+    def set_env_state(self, first, bins, items):
+        """Replace envs [first, first + len) for the next rollout
+        (xh_trainer_set_env_state)."""
+        bins = np.ascontiguousarray(bins, np.int8)
+        items = np.ascontiguousarray(items, np.int8)
+        count = bins.shape[0]
+        assert bins.shape == (count, self.B, self.D)
+        assert items.shape == (count, self.D)
+        check(_lib.lib.xh_trainer_set_env_state(self.h, first, count,
+                                                _ptr(bins), _ptr(items)))
+
     def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False,
                  init_items=None, trace_cap=0):
         """Argmax evaluation (deep_agent.cc / the drivers' periodic eval).

@@ -228,6 +228,81 @@ int xh_heuristic_evaluate(xh_ctx *ctx, int policy, int bins, int dims,
  * engine as a single reference worker does). */
 int xh_trainer_seed_streams(xh_trainer *t, uint32_t x);
 
+/* The state each env of the trainer starts its NEXT rollout step from (after
+ * learn() that is the batch's final state, which forget() keeps,
+ * rl.h:274-291): envs [first, first + count), bins int8 [count][B][D] and
+ * items int8 [count][D] (bp::environment::view, bin_packing.h:65).  set
+ * replaces it (a host-side apply / reset of that env between iterations);
+ * it never alters the current batch the learner reads. */
+int xh_trainer_get_env_state(xh_trainer *t, int first, int count, int8_t *bins,
+                             int8_t *items);
+int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
+                             const int8_t *bins, const int8_t *items);
+
+/* ------------------------------------------------- vectorised envs ---- */
+/* N bp::environment instances (bin_packing.h:46-85, generalised to B bins /
+ * D dims as the trainer's) whose state stays in HBM, for a caller that brings
+ * its own policy: xylo::environment<A,S>::apply / view / reset
+ * (rl.h:163-170) with the id parameter ranging over the whole batch, and
+ * xylo::agent::step minus the policy's react (rl.h:325-349) as ONE kernel for
+ * every env.
+ *
+ * Buffers (device memory owned by the venv; xh_venv_device_ptr gives the
+ * address for the caller's own kernels on the same device, xh_venv_get /
+ * xh_venv_set copy to / from host memory):
+ *   XH_VENV_ACTIONS int32 [N]        the chosen bin of every env (input)
+ *   XH_VENV_REWARD  f32   [N]        agent::get_reward of the last step
+ *   XH_VENV_DONE    uint8 [N]        agent::game_over after the last apply
+ *   XH_VENV_BINS    int8  [N][B][D]  bins (observation::bins)
+ *   XH_VENV_ITEMS   int8  [N][4]     item, D used (observation::item)
+ *   XH_VENV_RNG     uint32 [N]       per-env minstd_rand0 state
+ *   XH_VENV_OBS     f32   [N][B][2D] observation::to_vector (bin_packing.h:
+ *                                    31-40), written by xh_venv_observe and
+ *                                    by xh_venv_step(write_obs = 1)
+ *   XH_VENV_MASK    uint8 [N]        env selection for apply / reset
+ *
+ * Engine draws: construction 2 per env, get_item 2, reset 2.
+ * Env g of the job (env_offset + local index) starts on the global engine
+ * stream at x0, constructed in env order, and xh_venv_step reproduces the
+ * reference's draw order of a driver that steps every agent once per step in
+ * env order, its policy taking `policy_draws` draws per step (2 for the
+ * reference's discrete_action sampling and random_policy, 0 for a policy that
+ * draws nothing): step s of env g draws at 2 Ng + k (s Ng + g), k =
+ * policy_draws + 2.  xh_venv_apply / xh_venv_reset draw from the env's own
+ * stream where it stands (with Ng = 1 every call sequence is exactly the
+ * single-env reference engine).
+ *
+ * Calls are asynchronous on the context's stream; an out-of-range action
+ * leaves its env untouched and is reported by the next xh_venv_synchronize
+ * (or get) as XH_ERR_INVALID. */
+typedef struct xh_venv xh_venv;
+enum {
+  XH_VENV_ACTIONS = 0, XH_VENV_REWARD = 1, XH_VENV_DONE = 2,
+  XH_VENV_BINS = 3, XH_VENV_ITEMS = 4, XH_VENV_RNG = 5, XH_VENV_OBS = 6,
+  XH_VENV_MASK = 7, XH_VENV_BUF_COUNT
+};
+int xh_venv_create(xh_ctx *ctx, int num_envs, int bins, int dims,
+                   uint32_t rng_state, int env_offset, int num_envs_global,
+                   int policy_draws, xh_venv **out);
+int xh_venv_destroy(xh_venv *v);
+size_t xh_venv_bytes(const xh_venv *v, int which);
+void *xh_venv_device_ptr(xh_venv *v, int which);
+int xh_venv_get(xh_venv *v, int which, void *host, size_t bytes);
+int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes);
+/* agent::step minus react for every env: skip the policy's draws,
+ * environment::apply(ACTIONS[e]), REWARD / DONE, reset on game over;
+ * write_obs != 0 also writes OBS of the resulting states. */
+int xh_venv_step(xh_venv *v, int write_obs);
+/* environment::apply(ACTIONS[e], e) for the envs selected by MASK (all if
+ * use_mask == 0), no reset; DONE[e] = game_over after the apply. */
+int xh_venv_apply(xh_venv *v, int use_mask);
+/* environment::reset(e) for the envs selected by MASK (all if use_mask == 0). */
+int xh_venv_reset(xh_venv *v, int use_mask);
+/* observation::to_vector of every env into OBS. */
+int xh_venv_observe(xh_venv *v);
+/* Waits for the venv's work; XH_ERR_INVALID if an action was out of range. */
+int xh_venv_synchronize(xh_venv *v);
+
 /* sizeof of the ABI structs ("xh_config", "xh_eval"; 0 if unknown), so a
  * foreign-language binding can check its mirror of them. */
 size_t xh_struct_size(const char *name);

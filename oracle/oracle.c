@@ -162,6 +162,61 @@ void or_obs(const or_env_cfg *c, const int32_t *bins, const int32_t *item,
     }
 }
 
+/* A driver that steps Ng agents once per step in env order on ONE global
+ * engine (the sequential form of xylo::agent::step, rl.h:325-349, with a
+ * policy that draws `pd` engine values per react, e.g. 2 for
+ * discrete_action::from_vector, rl.h:27-30): construct env 0..Ng-1
+ * (bin_packing.h:50-52), then for each of S steps and each env: pd draws,
+ * apply(actions[s][g]), reward = game_over ? 0 : 1, reset on game over.
+ * Only envs [off, off + N) are recorded (actions given for those; the
+ * others' draws are consumed as a step of theirs would: pd + 2).
+ * Outputs: bins [S+1][N][B][D] and item [S+1][N][D] (state before step s,
+ * slot S = after the last), reward / done [S][N]; returns the engine state. */
+uint32_t or_venv_run(const or_env_cfg *c, int N, int Ng, int off, int pd,
+                     uint32_t x0, int S, const int32_t *actions, int32_t *bins,
+                     int32_t *item, float *reward, uint8_t *done) {
+  const int BD = c->B * c->D, D = c->D;
+  uint32_t x = x0;
+  int32_t *b = (int32_t *)malloc(sizeof(int32_t) * (size_t)N * BD);
+  int32_t *it = (int32_t *)calloc((size_t)N * 3, sizeof(int32_t));
+  int32_t *scratch_b = (int32_t *)malloc(sizeof(int32_t) * BD);
+  int32_t scratch_i[3];
+  for (int g = 0; g < Ng; ++g) {
+    const int local = g >= off && g < off + N;
+    or_env_construct(c, local ? b + (size_t)(g - off) * BD : scratch_b,
+                     local ? it + (size_t)(g - off) * 3 : scratch_i, &x);
+  }
+  for (int s = 0; s <= S; ++s) {
+    for (int e = 0; e < N; ++e) {
+      memcpy(bins + ((size_t)s * N + e) * BD, b + (size_t)e * BD,
+             sizeof(int32_t) * BD);
+      memcpy(item + ((size_t)s * N + e) * D, it + (size_t)e * 3,
+             sizeof(int32_t) * D);
+    }
+    if (s == S) break;
+    for (int g = 0; g < Ng; ++g) {
+      const int local = g >= off && g < off + N;
+      for (int k = 0; k < pd; ++k) (void)or_minstd_next(&x);
+      if (!local) {
+        (void)or_minstd_next(&x);
+        (void)or_minstd_next(&x);
+        continue;
+      }
+      const int e = g - off;
+      int32_t *eb = b + (size_t)e * BD, *ei = it + (size_t)e * 3;
+      or_env_apply(c, eb, ei, actions[(size_t)s * N + e], &x);
+      const int over = or_env_game_over(c, eb);
+      reward[(size_t)s * N + e] = over ? 0.0f : 1.0f;
+      done[(size_t)s * N + e] = (uint8_t)over;
+      if (over) or_env_reset(c, eb, ei, &x);
+    }
+  }
+  free(b);
+  free(it);
+  free(scratch_b);
+  return x;
+}
+
 /* ---------------------------------------------------------------- model -- */
 static int is_dense(int type) { return type == OR_FULL || type == OR_POINT; }
 

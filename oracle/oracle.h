@@ -55,6 +55,12 @@ int or_env_game_over(const or_env_cfg *c, const int32_t *bins);
 void or_obs(const or_env_cfg *c, const int32_t *bins, const int32_t *item,
             float *out);
 
+/* Sequential reference-order driver of Ng agents stepped once per step in
+ * env order (see oracle.c); the checker of the vectorised env (xh_venv). */
+uint32_t or_venv_run(const or_env_cfg *c, int N, int Ng, int off, int pd,
+                     uint32_t x0, int S, const int32_t *actions, int32_t *bins,
+                     int32_t *item, float *reward, uint8_t *done);
+
 /* ---------------------------------------------------------------- model -- */
 enum { OR_FULL = 0, OR_POINT = 1, OR_RELU = 2, OR_SOFTMAX = 3,
        OR_SOFTMAX_XENT = 4 };

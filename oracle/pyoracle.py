@@ -88,6 +88,11 @@ def lib():
         l.or_eval_argmax.restype = C.c_double
         l.or_eval_argmax.argtypes = [C.POINTER(EnvCfg), C.POINTER(Model),
                                      C.c_void_p, C.c_long, u32p]
+        l.or_venv_run.restype = C.c_uint32
+        l.or_venv_run.argtypes = [C.POINTER(EnvCfg), C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_uint32, C.c_int, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p]
         lib._l = l
     return lib._l
 
@@ -203,6 +208,25 @@ class Env:
         out = np.zeros(self.cfg.B * 2 * self.cfg.D, np.float32)
         lib().or_obs(C.byref(self.cfg), _ptr(self.bins), _ptr(self.item), _ptr(out))
         return out
+
+
+def venv_run(B, D, N, x0, actions, policy_draws=2, n_global=None, offset=0):
+    """or_venv_run: Ng agents stepped once per step in env order on one
+    engine seeded at state x0; actions [S][N] for envs [offset, offset + N).
+    Returns dict bins [S+1][N][B][D], item [S+1][N][D], reward / done [S][N],
+    x_end."""
+    actions = np.ascontiguousarray(actions, np.int32)
+    S = actions.shape[0]
+    cfg = env_cfg(B, D)
+    out = {"bins": np.zeros((S + 1, N, B, D), np.int32),
+           "item": np.zeros((S + 1, N, D), np.int32),
+           "reward": np.zeros((S, N), np.float32),
+           "done": np.zeros((S, N), np.uint8)}
+    out["x_end"] = lib().or_venv_run(
+        C.byref(cfg), N, n_global or N, offset, policy_draws, x0, S,
+        _ptr(actions), _ptr(out["bins"]), _ptr(out["item"]),
+        _ptr(out["reward"]), _ptr(out["done"]))
+    return out
 
 
 class Trainer:

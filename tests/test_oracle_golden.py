@@ -241,3 +241,24 @@ def test_heuristic_agents_match_reference(kind):
         assert np.float32(total / 1000.0) == g["round_avg"][r]
         if r == 0:
             np.testing.assert_array_equal(lens, g["episode_len"])
+
+
+def test_venv_driver_matches_reference():
+    """or_venv_run (the vectorised env's checker): one agent with a 2-draw
+    policy replays the reference's env8 trajectory given its choices, and a
+    shard of a many-env run equals that part of the whole run."""
+    g = golden("env8")
+    n = len(g["choice"])
+    out = po.venv_run(8, 2, 1, int(g["x0"][0]),
+                      np.asarray(g["choice"], np.int32).reshape(n, 1))
+    np.testing.assert_array_equal(out["bins"][:n, 0], g["start_bins"])
+    np.testing.assert_array_equal(out["item"][:n, 0], g["start_item"])
+    np.testing.assert_array_equal(out["reward"][:, 0], g["reward"])
+    assert out["x_end"] == int(g["x_end"][0])
+    rng = np.random.default_rng(3)
+    acts = rng.integers(0, 16, size=(6, 12)).astype(np.int32)
+    full = po.venv_run(16, 3, 12, 99, acts)
+    part = po.venv_run(16, 3, 4, 99, acts[:, 5:9], n_global=12, offset=5)
+    for k in ("bins", "item", "reward", "done"):
+        np.testing.assert_array_equal(part[k], full[k][:, 5:9])
+    assert part["x_end"] == full["x_end"]
