@@ -39,7 +39,8 @@ class Config(C.Structure):
         ("wd_policy", C.c_float), ("wd_value", C.c_float), ("gamma", C.c_float),
         ("lambda_", C.c_float), ("clip_eps", C.c_float),
         ("rng_state", C.c_uint32), ("kl_beta", C.c_float),
-        ("kl_target", C.c_float)]
+        ("kl_target", C.c_float), ("adv_normalize", C.c_int),
+        ("lr_scale_rows", C.c_int)]
 
 
 class Eval(C.Structure):

@@ -26,33 +26,87 @@ __global__ void value_targets_kernel(ValueArgs a, float gamma, float *targets) {
 
 // calculate_advantage (policy_gradient.h:220-281) on post-update values:
 // V(terminal end row) = 0, delta_t = r + gamma V' - V, A_t = sum_i
-// delta_i (lambda gamma)^(i-t) within the segment (forward sum, coefficient by
-// repeated multiplication, as the reference).
-__global__ void gae_kernel(ValueArgs a, float gamma, float lambda, float *adv) {
+// delta_i (lambda gamma)^(i-t) within the segment.  The reference's O(T^2)
+// forward sum is evaluated as the equivalent reverse recurrence A_t = delta_t
+// + lambda gamma A_{t+1} (A_t = delta_t on the terminal step), one env per
+// lane and no per-step arrays, so T is not bounded by registers (SURVEY
+// App. A.6: a reverse scan is allowed within tolerance).
+// part != nullptr (advantage normalisation, opt-in): the block's sum and sum
+// of squares of its advantages in double, reduced across the wave with
+// shuffles and across the block's waves in LDS, written to part[block][2].
+__global__ __launch_bounds__(256) void gae_kernel(ValueArgs a, float gamma,
+                                                  float lambda, float *adv,
+                                                  double *part) {
 #pragma clang fp contract(off)
   const int N = a.b.N, T = a.b.T;
+  const float lg = lambda * gamma;
+  double s1 = 0.0, s2 = 0.0;
   for (int env = blockIdx.x * blockDim.x + threadIdx.x; env < N;
        env += gridDim.x * blockDim.x) {
-    float delta[64];
-    int done[64];
-    for (int t = 0; t < T; ++t) {
+    float A = 0.0f;
+    for (int t = T - 1; t >= 0; --t) {
       const size_t q = (size_t)t * N + env;
-      done[t] = a.b.done[q];
-      const float reward = done[t] ? 0.0f : 1.0f;
-      const float vn = done[t] ? 0.0f : a.v_state[q + N];
-      delta[t] = reward + gamma * vn - a.v_state[q];
-    }
-    const float lg = lambda * gamma;
-    for (int t = 0; t < T; ++t) {
-      float A = 0.0f, coef = 1.0f;
-      for (int i = t; i < T; ++i) {
-        A += delta[i] * coef;
-        coef *= lg;
-        if (done[i]) break;
-      }
-      adv[(size_t)t * N + env] = A;
+      const int done = a.b.done[q];
+      const float reward = done ? 0.0f : 1.0f;
+      const float vn = done ? 0.0f : a.v_state[q + N];
+      const float delta = reward + gamma * vn - a.v_state[q];
+      A = done ? delta : delta + lg * A;
+      adv[q] = A;
+      s1 += (double)A;
+      s2 += (double)A * (double)A;
     }
   }
+  if (!part) return;
+  __shared__ double red[2][4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, kWave);
+    s2 += __shfl_xor(s2, o, kWave);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s1;
+    red[1][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+// Block partials -> stats[0..1] = (sum, sum of squares), a fixed-order
+// reduction in one wave (deterministic); all-reduced over ranks next.
+__global__ __launch_bounds__(64) void adv_stats_kernel(const double *part,
+                                                       int nparts,
+                                                       double *stats) {
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64) {
+    s1 += part[2 * i];
+    s2 += part[2 * i + 1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, kWave);
+    s2 += __shfl_xor(s2, o, kWave);
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = s1;
+    stats[1] = s2;
+  }
+}
+
+// A <- (A - mean) / (std + 1e-8) over the job's `count` transition rows
+// (population variance), evaluated in double and rounded once.
+__global__ void adv_normalize_kernel(float *adv, long n, const double *stats,
+                                     double count) {
+  const double mean = stats[0] / count;
+  double var = stats[1] / count - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const double inv = 1.0 / (sqrt(var) + 1e-8);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    adv[i] = (float)(((double)adv[i] - mean) * inv);
 }
 
 // Deterministic slab reduction: out[i] = sum over slabs in a fixed order.
@@ -130,10 +184,26 @@ hipError_t launch_value_targets(const ValueArgs &a, float gamma, float *targets,
   return hipGetLastError();
 }
 
+int gae_grid(int N) { return blocks_for(N, 256, 1024); }
+
 hipError_t launch_gae(const ValueArgs &a, float gamma, float lambda, float *adv,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(gae_kernel, dim3(blocks_for(a.b.N)), dim3(256), 0, s, a,
-                     gamma, lambda, adv);
+                      double *part, hipStream_t s) {
+  hipLaunchKernelGGL(gae_kernel, dim3(gae_grid(a.b.N)), dim3(256), 0, s, a,
+                     gamma, lambda, adv, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_adv_stats(const double *part, int nparts, double *stats,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(64), 0, s, part, nparts,
+                     stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_adv_normalize(float *adv, long n, const double *stats,
+                                double count, hipStream_t s) {
+  hipLaunchKernelGGL(adv_normalize_kernel, dim3(blocks_for(n)), dim3(256), 0, s,
+                     adv, n, stats, count);
   return hipGetLastError();
 }
 

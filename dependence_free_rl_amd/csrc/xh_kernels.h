@@ -267,8 +267,15 @@ int rollout_grid(int B, int D, int H1, int H2);
 bool value_shape_supported(int V1, int V2);
 hipError_t launch_value_targets(const ValueArgs &a, float gamma, float *targets,
                                 hipStream_t s);
+// GAE; part != nullptr also writes per-block (sum, sum of squares) of the
+// advantages for the opt-in normalisation ([gae_grid(N)][2] doubles).
+int gae_grid(int N);
 hipError_t launch_gae(const ValueArgs &a, float gamma, float lambda, float *adv,
-                      hipStream_t s);
+                      double *part, hipStream_t s);
+hipError_t launch_adv_stats(const double *part, int nparts, double *stats,
+                            hipStream_t s);
+hipError_t launch_adv_normalize(float *adv, long n, const double *stats,
+                                double count, hipStream_t s);
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s);
 hipError_t launch_sgd(float *params, const float *grad, int n, float lr,

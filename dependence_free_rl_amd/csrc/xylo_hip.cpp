@@ -133,6 +133,7 @@ struct xh_trainer {
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
   float *logits = nullptr, *probs = nullptr;
+  double *adv_part = nullptr, *adv_stats = nullptr;  // adv_normalize
   // KL-PPO state
   float *qold = nullptr, *beta = nullptr, *kl_log = nullptr;
   int *end_list = nullptr, *n_end = nullptr, *n_open = nullptr;
@@ -325,6 +326,21 @@ void *buffer_ptr(const xh_trainer *t, int which) {
   return nullptr;
 }
 
+// Copies between the device and caller (pageable) host memory: drain the
+// stream, then a blocking hipMemcpy.  An asynchronous copy into or out of
+// pageable memory is staged by the runtime, and reading the host array right
+// after the stream synchronisation was measured to return stale entries on
+// ROCm 7.2 (evaluate traces differing between identical calls).
+hipError_t copy_to_host(void *host, const void *dev, size_t n, hipStream_t s) {
+  const hipError_t e = hipStreamSynchronize(s);
+  return e != hipSuccess ? e : hipMemcpy(host, dev, n, hipMemcpyDeviceToHost);
+}
+hipError_t copy_to_device(void *dev, const void *host, size_t n,
+                          hipStream_t s) {
+  const hipError_t e = hipStreamSynchronize(s);
+  return e != hipSuccess ? e : hipMemcpy(dev, host, n, hipMemcpyHostToDevice);
+}
+
 int copy_ok(hipError_t e) {
   return e == hipSuccess ? XH_OK
                          : fail(XH_ERR_HIP, "copy: %s", hipGetErrorString(e));
@@ -399,8 +415,8 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
   int st = XH_OK;
   if (e->init_items) {
     eb.init_items = (const int *)(scratch + o_init);
-    st = copy_ok(hipMemcpyAsync(scratch + o_init, e->init_items,
-                                4 * (size_t)n * D, hipMemcpyHostToDevice, s));
+    st = copy_ok(copy_to_device(scratch + o_init, e->init_items,
+                                4 * (size_t)n * D, s));
   }
   // from here on a failure is recorded in `st` and the scratch block, the
   // events and the stream are still released / drained below
@@ -417,8 +433,7 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
   }
   auto out = [&](void *host, size_t off, size_t nb) {
     if (st == XH_OK && host)
-      st = copy_ok(hipMemcpyAsync(host, scratch + off, nb,
-                                  hipMemcpyDeviceToHost, s));
+      st = copy_ok(copy_to_host(host, scratch + off, nb, s));
   };
   out(e->totals, 0, sizeof(double) * n);
   out(e->steps, o_steps, 8 * (size_t)n);
@@ -440,11 +455,17 @@ int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
               int n) {
   hipStream_t s = t->ctx->stream;
   auto &o = t->opt[which];
+  // lr_scale_rows (opt-in): lr / rows of the job instead of the raw lr on
+  // the row-summed gradient (nn.h:94-98, 624)
+  const float lr = t->cfg.lr_scale_rows
+                       ? (float)((double)o.lr /
+                                 ((double)t->T() * t->cfg.num_envs_global))
+                       : o.lr;
   if (o.kind == XH_OPT_SGD)
     return timed(t, "reduce_sgd", [&]() {
-      return xh::launch_sgd(params, grad, n, o.lr, o.wd, s);
+      return xh::launch_sgd(params, grad, n, lr, o.wd, s);
     });
-  xh::OptStep st{o.kind, o.lr, o.beta1, o.beta2, 1.0f, 1.0f};
+  xh::OptStep st{o.kind, lr, o.beta1, o.beta2, 1.0f, 1.0f};
   if (o.kind == XH_OPT_ADAM) {  // host float powf, as the reference
     st.c1 = 1 - powf(o.beta1, o.t);
     st.c2 = 1 - powf(o.beta2, o.t);
@@ -467,12 +488,10 @@ int apply_env_overrides(xh_trainer *t) {
   const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
   for (auto &kv : t->env_override) {
     const size_t e = (size_t)kv.first;
-    HIPCHK(hipMemcpyAsync(t->bins + e * BD, kv.second.data(), BD,
-                          hipMemcpyHostToDevice, s));
+    HIPCHK(copy_to_device(t->bins + e * BD, kv.second.data(), BD, s));
     int8_t it[4] = {0, 0, 0, 0};
     for (size_t d = 0; d < D; ++d) it[d] = kv.second[BD + d];
-    HIPCHK(hipMemcpyAsync(t->items + e * 4, it, 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));  // `it` is a stack buffer
+    HIPCHK(copy_to_device(t->items + e * 4, it, 4, s));
   }
   t->env_override.clear();
   return XH_OK;
@@ -570,8 +589,21 @@ int do_learn(xh_trainer *t) {
   va.v_state = t->v_state;
   va.row_g = nullptr;
   CHK(timed(t, "value", [&]() {
-    return xh::launch_gae(va, c.gamma, c.lambda, t->adv, s);
+    return xh::launch_gae(va, c.gamma, c.lambda, t->adv,
+                          c.adv_normalize ? t->adv_part : nullptr, s);
   }));
+  if (c.adv_normalize) {  // opt-in: job-wide mean / std of the advantages
+    CHK(timed(t, "value", [&]() {
+      return xh::launch_adv_stats(t->adv_part, xh::gae_grid((int)t->N()),
+                                  t->adv_stats, s);
+    }));
+    CHK(allreduce_d(t, t->adv_stats, 2));
+    CHK(timed(t, "value", [&]() {
+      return xh::launch_adv_normalize(t->adv, (long)(t->T() * t->N()),
+                                      t->adv_stats,
+                                      (double)t->T() * c.num_envs_global, s);
+    }));
+  }
   // optimize_action: k policy steps (policy_gradient.h:297-307)
   xh::PolicyTrainArgs pa{};
   pa.env = t->env;
@@ -674,6 +706,10 @@ xh::MlpArgs pg_mlp(const xh_trainer *t, bool learn, int slot) {
 }
 
 int create_pg(xh_ctx *ctx, const xh_config &c, xh_trainer **out) {
+  if (c.adv_normalize || c.lr_scale_rows)
+    return fail(XH_ERR_INVALID, "REINFORCE: adv_normalize / lr_scale_rows are "
+                "actor-critic / PPO options (REINFORCE has its own mean-return "
+                "baseline, policy_gradient.h:125-147)");
   if (c.bins < 2 || c.bins > 128 || c.dims < 1 || c.dims > 3)
     return fail(XH_ERR_INVALID, "REINFORCE: bins %d (2..128), dims %d (1..3)",
                 c.bins, c.dims);
@@ -986,8 +1022,7 @@ int xh_ctx_allreduce_host(xh_ctx *c, float *data, size_t n) {
     float *d = nullptr;
     HIPCHK(hipMalloc(&d, n * sizeof(float)));
     // the device buffer is freed on every path (the stream drained first)
-    int st = copy_ok(hipMemcpyAsync(d, data, n * sizeof(float),
-                                    hipMemcpyHostToDevice, c->stream));
+    int st = copy_ok(copy_to_device(d, data, n * sizeof(float), c->stream));
     if (st == XH_OK) {
       const ncclResult_t r =
           ncclAllReduce(d, d, n, ncclFloat32, ncclSum, c->comm, c->stream);
@@ -995,8 +1030,7 @@ int xh_ctx_allreduce_host(xh_ctx *c, float *data, size_t n) {
         st = fail(XH_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     }
     if (st == XH_OK)
-      st = copy_ok(hipMemcpyAsync(data, d, n * sizeof(float),
-                                  hipMemcpyDeviceToHost, c->stream));
+      st = copy_ok(copy_to_host(data, d, n * sizeof(float), c->stream));
     const hipError_t se = hipStreamSynchronize(c->stream);
     if (st == XH_OK && se != hipSuccess)
       st = fail(XH_ERR_HIP, "synchronize: %s", hipGetErrorString(se));
@@ -1060,8 +1094,8 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     if (c.num_envs <= 0 || c.num_envs % G)
       return fail(XH_ERR_INVALID, "num_envs %d must be a positive multiple of %d",
                   c.num_envs, G);
-    if (c.steps < 1 || c.steps > 64)
-      return fail(XH_ERR_INVALID, "steps %d not in [1,64]", c.steps);
+    if (c.steps < 1 || c.steps > 1024)
+      return fail(XH_ERR_INVALID, "steps %d not in [1,1024]", c.steps);
     if (c.epochs < 1 || c.epochs > 64)
       return fail(XH_ERR_INVALID, "epochs %d", c.epochs);
     if (c.num_envs_global < c.num_envs || c.env_offset < 0 ||
@@ -1124,6 +1158,10 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->vgrad, (size_t)t->nv * 4);
     A(&t->logits, N * c.bins * 4);
     A(&t->probs, N * c.bins * 4);
+    if (c.adv_normalize) {
+      A(&t->adv_part, (size_t)xh::gae_grid((int)N) * 2 * 8);
+      A(&t->adv_stats, 2 * 8);
+    }
     if (c.algo == XH_KLPPO) {
       A(&t->qold, T * N * c.bins * 4);
       A(&t->beta, 4);
@@ -1203,8 +1241,7 @@ int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
                   want);
     HIPCHK(hipSetDevice(t->ctx->device));
     float *dst = which == XH_POLICY ? t->pp : t->vp;
-    HIPCHK(hipMemcpyAsync(dst, host, n * 4, hipMemcpyHostToDevice,
-                          t->ctx->stream));
+    HIPCHK(copy_to_device(dst, host, n * 4, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     return XH_OK;
   });
@@ -1218,8 +1255,8 @@ int xh_trainer_get_params(xh_trainer *t, int which, float *host, size_t n) {
       return fail(XH_ERR_INVALID, "params: got %zu floats, model has %zu", n,
                   want);
     HIPCHK(hipSetDevice(t->ctx->device));
-    HIPCHK(hipMemcpyAsync(host, which == XH_POLICY ? t->pp : t->vp, n * 4,
-                          hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHK(copy_to_host(host, which == XH_POLICY ? t->pp : t->vp, n * 4,
+                        t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     return XH_OK;
   });
@@ -1313,8 +1350,7 @@ int xh_trainer_set_forced_actions(xh_trainer *t, const int32_t *host) {
       if (host[i] < 0 || host[i] >= t->cfg.bins)
         return fail(XH_ERR_INVALID, "forced action %d out of range", host[i]);
     HIPCHK(hipSetDevice(t->ctx->device));
-    HIPCHK(hipMemcpyAsync(t->forced, host, n * 4, hipMemcpyHostToDevice,
-                          t->ctx->stream));
+    HIPCHK(copy_to_device(t->forced, host, n * 4, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     t->use_forced = true;
     return XH_OK;
@@ -1333,8 +1369,7 @@ int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes) {
       return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
                   bytes, want);
     HIPCHK(hipSetDevice(t->ctx->device));
-    HIPCHK(hipMemcpyAsync(host, buffer_ptr(t, which), bytes,
-                          hipMemcpyDeviceToHost, t->ctx->stream));
+    HIPCHK(copy_to_host(host, buffer_ptr(t, which), bytes, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     return XH_OK;
   });
@@ -1355,8 +1390,7 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
           return fail(XH_ERR_INVALID, "action %d out of range", a[i]);
     }
     HIPCHK(hipSetDevice(t->ctx->device));
-    HIPCHK(hipMemcpyAsync(buffer_ptr(t, which), host, bytes,
-                          hipMemcpyHostToDevice, t->ctx->stream));
+    HIPCHK(copy_to_device(buffer_ptr(t, which), host, bytes, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     if (which == XH_BUF_BINS || which == XH_BUF_ITEMS) t->need_shift = false;
     return XH_OK;
@@ -1493,10 +1527,10 @@ int xh_trainer_get_env_state(xh_trainer *t, int first, int count, int8_t *bins,
     const size_t BD = t->BD(), D = (size_t)t->cfg.dims, N = t->N();
     const size_t slot = t->need_shift ? t->T() : 0;
     std::vector<int8_t> it((size_t)count * 4);
-    HIPCHK(hipMemcpyAsync(bins, t->bins + (slot * N + first) * BD,
-                          (size_t)count * BD, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(it.data(), t->items + (slot * N + first) * 4,
-                          (size_t)count * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(copy_to_host(bins, t->bins + (slot * N + first) * BD,
+                        (size_t)count * BD, s));
+    HIPCHK(copy_to_host(it.data(), t->items + (slot * N + first) * 4,
+                        (size_t)count * 4, s));
     HIPCHK(hipStreamSynchronize(s));
     for (int e = 0; e < count; ++e) {
       auto o = t->env_override.find(first + e);
@@ -1626,7 +1660,7 @@ void *xh_venv_device_ptr(xh_venv *v, int which) {
 namespace {
 int venv_check_err(xh_venv *v) {
   int err = 0;
-  HIPCHK(hipMemcpyAsync(&err, v->err, 4, hipMemcpyDeviceToHost, v->ctx->stream));
+  HIPCHK(copy_to_host(&err, v->err, 4, v->ctx->stream));
   HIPCHK(hipStreamSynchronize(v->ctx->stream));
   if (err) {
     HIPCHK(hipMemset(v->err, 0, 4));
@@ -1657,8 +1691,7 @@ int xh_venv_get(xh_venv *v, int which, void *host, size_t bytes) {
       return fail(XH_ERR_INVALID, "venv buffer %d: %zu bytes, expected %zu",
                   which, bytes, xh_venv_bytes(v, which));
     HIPCHK(hipSetDevice(v->ctx->device));
-    HIPCHK(hipMemcpyAsync(host, v->buf[which], bytes, hipMemcpyDeviceToHost,
-                          v->ctx->stream));
+    HIPCHK(copy_to_host(host, v->buf[which], bytes, v->ctx->stream));
     return venv_check_err(v);
   });
 }
@@ -1683,8 +1716,7 @@ int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes) {
           return fail(XH_ERR_INVALID, "venv: bin value %d above capacity", b[i]);
     }
     HIPCHK(hipSetDevice(v->ctx->device));
-    HIPCHK(hipMemcpyAsync(v->buf[which], host, bytes, hipMemcpyHostToDevice,
-                          v->ctx->stream));
+    HIPCHK(copy_to_device(v->buf[which], host, bytes, v->ctx->stream));
     HIPCHK(hipStreamSynchronize(v->ctx->stream));
     return XH_OK;
   });

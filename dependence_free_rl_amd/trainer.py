@@ -171,7 +171,8 @@ class Trainer:
                  widths=(128, 128), value_widths=(64, 32), epochs=None,
                  lr_policy=None, lr_value=None, wd_policy=None, wd_value=None,
                  gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
-                 num_envs_global=None, env_offset=0):
+                 num_envs_global=None, env_offset=0, adv_normalize=False,
+                 lr_scale_rows=False):
         cfg = _lib.Config()
         a = ALGOS[algo]
         _lib.lib.xh_config_default(C.byref(cfg), a, bins, dims, num_envs, steps)
@@ -191,6 +192,9 @@ class Trainer:
             cfg.wd_value = wd_value
         cfg.gamma, cfg.lambda_, cfg.clip_eps = gamma, lam, clip_eps
         cfg.rng_state = rng_state
+        # opt-in, off in the reference configuration (xh_config)
+        cfg.adv_normalize = int(bool(adv_normalize))
+        cfg.lr_scale_rows = int(bool(lr_scale_rows))
         self.cfg = cfg
         self.ctx = ctx
         self.B, self.D, self.N, self.T = bins, dims, num_envs, steps

@@ -88,7 +88,8 @@ typedef struct {
   int num_envs_global; /* envs in the whole job (reference-order RNG streams) */
   int env_offset;      /* global index of this rank's first env              */
   int bins, dims;      /* B (bin_packing.h:12 num_bins), D (2 in the ref)    */
-  int steps;           /* T: env steps per env per iteration (play_steps(T)) */
+  int steps;           /* T: env steps per env per iteration (play_steps(T));
+                          1..1024 (REINFORCE: episodes per env, 1..64)     */
   int epochs;          /* PPO / KL-PPO k (policy_gradient.h:300), 1 for AC  */
   int policy_h1, policy_h2; /* per-bin conv1d_1 widths                       */
   int value_h1, value_h2;   /* value full_layer widths (64, 32)              */
@@ -99,6 +100,15 @@ typedef struct {
   uint32_t rng_state;  /* minstd_rand0 state before the envs are constructed */
   float kl_beta;       /* KL-PPO initial beta (1, policy_gradient.h:332)     */
   float kl_target;     /* KL-PPO d_targ (1e-9, policy_gradient.h:333)        */
+  /* Opt-in options, both 0 (off) in the reference-parity configuration:   */
+  int adv_normalize;   /* 1: after GAE, A <- (A - mean) / (std + 1e-8) over
+                          the job's T * num_envs_global transitions (the
+                          reference normalises nothing, policy_gradient.h:
+                          220-281); statistics by wave reductions, summed
+                          across ranks */
+  int lr_scale_rows;   /* 1: both optimizers apply lr / rows, rows = T *
+                          num_envs_global, i.e. SGD on the mean instead of the
+                          reference's sum over rows (nn.h:94-98, 624) */
 } xh_config;
 
 /* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */

@@ -505,6 +505,8 @@ struct or_trainer {
   or_opt opt[2];      /* policy, value optimizers */
   uint32_t x, x0;
   uint32_t *xs;       /* per-env streams (or_trainer_set_env_streams) */
+  int adv_normalize;  /* opt-in options (or_trainer_set_options) */
+  int lr_scale_rows;
   /* workers */
   int32_t *bins, *item; /* N*B*D, N*D */
   int *steps;
@@ -636,6 +638,21 @@ void or_trainer_set_optimizer(or_trainer *t, int which, int kind, float lr,
 }
 
 uint32_t or_trainer_rng(const or_trainer *t) { return t->x; }
+
+void or_trainer_set_options(or_trainer *t, int adv_normalize,
+                            int lr_scale_rows) {
+  t->adv_normalize = adv_normalize;
+  t->lr_scale_rows = lr_scale_rows;
+}
+
+/* optimizer step with the opt-in lr / rows scaling (rows = T * N) */
+static void opt_step_scaled(or_trainer *t, or_opt *o, float *params,
+                            const float *grad, size_t n) {
+  const float lr = o->lr;
+  if (t->lr_scale_rows) o->lr = (float)((double)lr / ((double)t->T * t->N));
+  or_opt_step(o, params, grad, n);
+  o->lr = lr;
+}
 
 /* Independent per-env streams: env i draws from x0 advanced by i * stride
  * (the device evaluators' and REINFORCE trainer's convention; env 0 is the
@@ -978,7 +995,7 @@ void or_trainer_learn(or_trainer *t) {
     sq_ctx sc = {targets};
     or_model_grad(&t->val, t->vp, sm, rows, len, loss_square, &sc, vgrad);
     buf_set(&t->buf[OR_BUF_VALUE_GRAD], vgrad, t->nv, sizeof(float));
-    or_opt_step(&t->opt[1], t->vp, vgrad, t->nv);
+    opt_step_scaled(t, &t->opt[1], t->vp, vgrad, t->nv);
     free(vgrad);
 
     /* calculate_advantage (policy_gradient.h:220-281), post-update values */
@@ -1021,6 +1038,24 @@ void or_trainer_learn(or_trainer *t) {
     free(deltas);
     free(values);
     free(targets);
+    if (t->adv_normalize) {
+      /* opt-in (not in the reference): over the transition rows, population
+       * statistics in double, A <- (A - mean) / (std + 1e-8) rounded once;
+       * end rows keep A = 0 */
+      double s1 = 0.0, s2 = 0.0, cnt = 0.0;
+      for (int i = 0; i < rows; ++i)
+        if (!rend[i]) {
+          s1 += adv[i];
+          s2 += (double)adv[i] * adv[i];
+          cnt += 1.0;
+        }
+      const double mean = s1 / cnt;
+      double var = s2 / cnt - mean * mean;
+      if (var < 0) var = 0;
+      const double inv = 1.0 / (sqrt(var) + 1e-8);
+      for (int i = 0; i < rows; ++i)
+        if (!rend[i]) adv[i] = (float)(((double)adv[i] - mean) * inv);
+    }
 
     /* optimize_action: PPO k=4 surrogate steps (policy_gradient.h:297-307),
      * AC one policy_loss step (:187-194) */
@@ -1040,7 +1075,7 @@ void or_trainer_learn(or_trainer *t) {
         const float kl[3] = {beta_used, (float)pc.d_avg, t->beta};
         buf_append(&t->buf[OR_BUF_KL], kl, 3, sizeof(float));
       }
-      or_opt_step(&t->opt[0], t->pp, pgrad, t->np);
+      opt_step_scaled(t, &t->opt[0], t->pp, pgrad, t->np);
     }
   }
   buf_set(&t->buf[OR_BUF_ADVANTAGES], adv, rows, sizeof(float));

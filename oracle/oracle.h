@@ -114,6 +114,11 @@ void or_trainer_set_optimizer(or_trainer *t, int which, int kind, float lr,
  * engine draws are still consumed). */
 void or_trainer_rollout(or_trainer *t, const int32_t *forced);
 void or_trainer_learn(or_trainer *t); /* learn() + replay_buffer.forget() */
+/* Opt-in options of the device trainer (xh_config.adv_normalize /
+ * lr_scale_rows; not in the reference): advantage normalisation over the
+ * transition rows, and lr / (T * N) for both optimizers.  AC / PPO only. */
+void or_trainer_set_options(or_trainer *t, int adv_normalize,
+                            int lr_scale_rows);
 uint32_t or_trainer_rng(const or_trainer *t);
 /* Per-env streams: env i draws from x0 advanced by i * stride (env 0 = the
  * single-env reference run), re-constructing the envs on those streams; or,

@@ -88,6 +88,7 @@ def lib():
         l.or_eval_argmax.restype = C.c_double
         l.or_eval_argmax.argtypes = [C.POINTER(EnvCfg), C.POINTER(Model),
                                      C.c_void_p, C.c_long, u32p]
+        l.or_trainer_set_options.argtypes = [C.c_void_p, C.c_int, C.c_int]
         l.or_venv_run.restype = C.c_uint32
         l.or_venv_run.argtypes = [C.POINTER(EnvCfg), C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_uint32, C.c_int, C.c_void_p,
@@ -260,6 +261,10 @@ class Trainer:
                                                C.c_float, C.c_float, C.c_float,
                                                C.c_float]
         l.or_trainer_set_optimizer(self.h, which, kind, lr, wd, beta1, beta2)
+
+    def set_options(self, adv_normalize=False, lr_scale_rows=False):
+        lib().or_trainer_set_options(self.h, int(adv_normalize),
+                                     int(lr_scale_rows))
 
     def set_env_streams(self, stride=1 << 26, reconstruct=True):
         """Env i on its own stream: x0 advanced by i * stride (reconstructing
