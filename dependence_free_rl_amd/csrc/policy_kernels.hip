@@ -57,6 +57,12 @@ struct PShape {
   static constexpr int FJ = NOT >= 4 ? 2 : 1;  // fwd r-tiles per wave
   static constexpr int JW = (NOT * NIT + 3) / 4;  // dW2 tiles per wave
   static constexpr int JH = (2 * NIT + 3) / 4;    // dH1 r-tiles per wave
+  // 4-wave train kernel: workgroups per CU it is compiled for.  The 1-D
+  // [64,64] shape (config 2) fits 256 VGPRs without scratch, so two
+  // workgroups share a CU and one's barrier / softmax phases overlap the
+  // other's MFMAs; the wider shapes need the full register file (spills
+  // measured at 2).
+  static constexpr int TOCC = (H1 <= 64 && H2 <= 64 && D == 1) ? 2 : 1;
   static_assert(B == 8 || B == 16 || B == 32 || B == 64 || B == 128, "B");
   static_assert(NIT == 1 || NIT == 2 || NIT == 4, "H1 in {32,64,128}");
   static_assert(NOT == 1 || NOT == 2 || NOT == 4, "H2 in {32,64,128}");
@@ -732,7 +738,7 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
 // overflowed view, rl.h:336-343); end rows have A = 0 and the previous
 // action's distribution (policy_gradient.h:178).
 template <class S, bool KL>
-__global__ __launch_bounds__(256, 1) void policy_train_kernel(PolicyTrainArgs a) {
+__global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
   __syncthreads();
@@ -1524,7 +1530,14 @@ int rollout_grid(int B, int D, int H1, int H2) {
   return 2 * cu_count();
 }
 int policy_train_grid(int B, int D, int H1, int H2) {
-  (void)B; (void)D; (void)H1; (void)H2;
+#define X(XB, XD, XH1, XH2)                                     \
+  if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {          \
+    using S = PShape<XB, XD, XH1, XH2>;                         \
+    return (S::NIT == 4 && S::NOT == 4) ? cu_count()            \
+                                        : S::TOCC * cu_count(); \
+  }
+  XH_POLICY_SHAPES(X)
+#undef X
   return cu_count();
 }
 

@@ -393,13 +393,19 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
                     "an item of the table", i, e->init_items[i]);
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  const size_t o_steps = sizeof(double) * n, o_rng = o_steps + 8 * (size_t)n,
-               o_init = o_rng + 4 * (size_t)n,
-               o_fin = o_init + 4 * (size_t)n * D,
-               o_trace = o_fin + 4 * (size_t)n * D,
-               bytes = o_trace + 4 * (size_t)(e->trace ? e->trace_cap : 0);
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_steps = up(sizeof(double) * n),
+               o_rng = o_steps + up(8 * (size_t)n),
+               o_init = o_rng + up(4 * (size_t)n),
+               o_fin = o_init + up(4 * (size_t)n * D),
+               o_trace = o_fin + up(4 * (size_t)n * D),
+               bytes = o_trace + up(4 * (size_t)(e->trace ? e->trace_cap : 0));
+  // a plain device allocation, each region on its own 256-byte boundary
+  // (the stream-ordered allocator returned trace bytes that read back wrong
+  // for some sizes on ROCm 7.2: measured at trace_cap 2049 and 10000)
   char *scratch = nullptr;
-  HIPCHK(hipMallocAsync((void **)&scratch, bytes, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMalloc((void **)&scratch, bytes));
   EvalBuffers eb{};
   const uint32_t x0 = e->rng_state % 2147483647u;
   eb.x0 = x0 ? x0 : 1u;
@@ -440,7 +446,8 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
   out(e->rng_out, o_rng, 4 * (size_t)n);
   out(e->final_items, o_fin, 4 * (size_t)n * D);
   out(e->trace, o_trace, 4 * (size_t)eb.trace_cap);
-  (void)hipFreeAsync(scratch, s);
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(scratch);
   hip_ok(hipStreamSynchronize(s), "synchronize");
   float ms = 0.0f;
   if (st == XH_OK && hipEventElapsedTime(&ms, ev0, ev1) == hipSuccess)

@@ -1,4 +1,4 @@
-"""Diagnostic: determinism of evaluate() (one call vs repeated, chained)."""
+"""Diagnostic: evaluate() traces across trace_cap values."""
 import sys
 import numpy as np
 sys.path.insert(0, ".")
@@ -12,26 +12,23 @@ g = golden("deep_w20")
 tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1, widths=(128, 64))
 tr.set_params(POLICY, g["params"])
 x0 = int(g["x0"][0])
-ref = None
-for rep in range(4):
-    w = tr.evaluate(8, 1000, x0, trace_cap=30000)
-    if ref is None:
-        ref = w
-    d = np.nonzero(w["trace"] != ref["trace"])[0]
-    print("whole", rep, w["totals"], w["steps"][0], w["rng"][0], "trace diff", d[:4], len(d))
-for rep in range(3):
-    rng = po.Rng(x0)
-    first = rng.canonical() < 0.4
-    item = [4, 2] if first else [1, 2]
-    x, tot, n = po.minstd_jump(x0, 2), 0.0, 0
-    tr_all = []
-    for c in range(10):
-        r = tr.evaluate(8, 100, x, init_items=np.tile(item, (8, 1)), trace_cap=3000)
-        k = int(r["steps"][0])
-        tr_all.append(r["trace"][:k])
-        tot += r["totals"][0]
-        n += k
-        x, item = int(r["rng"][0]), list(r["final_items"][0])
-    t = np.concatenate(tr_all)
-    d = np.nonzero(t != ref["trace"][:len(t)])[0]
-    print("chained", rep, tot, n, x, "trace diff vs whole", d[:4], len(d))
+w = tr.evaluate(8, 100, x0, trace_cap=3000)
+rng = po.Rng(x0)
+first = rng.canonical() < 0.4
+item = [4, 2] if first else [1, 2]
+x = po.minstd_jump(x0, 2)
+bad = 0
+for cap in (1, 7, 2048, 2049, 3000, 4096, 10000, 12345):
+    for init in (None, np.tile(item, (8, 1))):
+        r2 = tr.evaluate(8, 100, x0 if init is None else x, init_items=init, trace_cap=cap)
+        k = min(cap, 2748)
+        d = np.nonzero(r2["trace"][:k] != w["trace"][:k])[0]
+        bad += len(d)
+        print(cap, init is None, r2["totals"][0], d[:5])
+whole = tr.evaluate(8, 1000, x0)
+x, tot = po.minstd_jump(x0, 2), 0.0
+for _ in range(10):
+    r = tr.evaluate(8, 100, x, init_items=np.tile(item, (8, 1)))
+    tot += r["totals"][0]
+    x, item = int(r["rng"][0]), list(r["final_items"][0])
+print("chained", tot, whole["totals"][0], "BAD" if bad or tot != whole["totals"][0] else "OK")
