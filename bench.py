@@ -118,19 +118,21 @@ def pmc_traffic(kernel="policy_train"):
     kernel's reads are narrow int8 loads, for which the gfx950 x2 correction
     of wide streaming reads does not apply)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        summ = json.load(f)
-    # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
+    # newest round first (profiles/<round><pass>[_c<config>]_pmc_summary.json);
     # only a summary of this very shape counts (PShape<B, D, H1, H2>)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")),
+                   reverse=True)
     shape = "PShape<%d, %d, %d, %d>" % (B, D, H1, H2)
-    s = next((v for k, v in sorted(summ.items())
-              if k.startswith(kernel) and shape in v.get("kernel", "")), None)
-    if not s:
-        return None, None
-    return s["hbm_bytes"], os.path.relpath(files[-1], REPO)
+    for path in files:
+        with open(path) as f:
+            summ = json.load(f)
+        # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
+        s = next((v for k, v in sorted(summ.items())
+                  if k.startswith(kernel) and shape in v.get("kernel", "")
+                  and "hbm_bytes" in v), None)
+        if s:
+            return s["hbm_bytes"], os.path.relpath(path, REPO), s
+    return None, None, None
 
 
 def main():
@@ -205,7 +207,7 @@ def main():
     # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
     avg_ms = ms_pt / max(n_pt, 1)
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src, pmc = pmc_traffic()
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
@@ -249,6 +251,8 @@ def main():
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
                      "traffic_source": traffic_src,
+                     "mfma_busy_frac": pmc and pmc.get("mfma_busy_frac"),
+                     "clock_ghz_profiled": pmc and pmc.get("clock_ghz"),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
                      "flops_per_launch": flops_epoch},

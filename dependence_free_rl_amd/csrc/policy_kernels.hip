@@ -1234,7 +1234,9 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
 #pragma unroll
     for (int hg = 0; hg < HG; ++hg) {
       if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
-      pre = forward(HG == 1);
+      // the last half-group's H1 image is written here and its pre-
+      // activations stay in registers for the backward
+      pre = forward(hg == HG - 1);
       const float zp = logit_part<S, true>(lds, pre, q);
       if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
     }
@@ -1306,10 +1308,14 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       }
     }
 
+    // backward, last half-group first: it reuses the forward's registers and
+    // H1 image; the earlier half-groups recompute their forward (a second
+    // 64-row H1 image does not fit in LDS beside W2 and the dA2 image)
 #pragma unroll
-    for (int hg = 0; hg < HG; ++hg) {
-      if (HG > 1) {  // recompute this half-group's forward (no room to keep it)
-        if (hg > 0) __syncthreads();  // previous half-group's images consumed
+    for (int hb = 0; hb < HG; ++hb) {
+      const int hg = HG - 1 - hb;
+      if (hb > 0) {
+        __syncthreads();  // previous half-group's images consumed
         fetch_row(g, hg, bv_c, iv_c);
         pre = forward(true);
       }

@@ -44,10 +44,10 @@ def test_flops_match_survey_8d(bench):
 
 def test_pmc_traffic_only_for_the_same_shape(bench):
     bench.select_config(3)
-    t, src = bench.pmc_traffic()
+    t, src, _ = bench.pmc_traffic()
     if t is not None:  # a committed summary of the 64-bin shape
         assert src.startswith("profiles/") and t > 0
     bench.select_config(5)
-    t5, _ = bench.pmc_traffic()
+    t5, _, _ = bench.pmc_traffic()
     # never the 64-bin kernel's counters for the 128-bin shape
     assert t5 is None or t5 != t

@@ -34,7 +34,16 @@ def short(name):
     return m.group(1) if m else name
 
 
-def main(tag, trace, fetch, write):
+def per_kernel_all(path):
+    """{kernel: {counter: mean value per dispatch}} of a --pmc pass."""
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+
+
+def main(tag, trace, fetch, write, *sq_dirs):
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.environ.get("PROFILE_OUT", os.path.join(here, "profiles"))
     os.makedirs(out, exist_ok=True)
@@ -49,6 +58,21 @@ def main(tag, trace, fetch, write):
         summary[short(k)] = {"kernel": k, "avg_ns": dur.get(k), "fetch_bytes_raw": fb,
                       "fetch_bytes_x2": 2 * fb, "write_bytes": wb,
                       "hbm_bytes": fb + wb, "hbm_bytes_x2_reads": 2 * fb + wb}
+    # SQ / GRBM passes (MFMA utilisation): raw per-dispatch means, plus
+    #   clock_ghz       = GRBM_GUI_ACTIVE / 8 XCDs / duration
+    #   mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024
+    #                     SIMDs): share of SIMD-cycles the matrix pipe was busy
+    for d in sq_dirs:
+        for k, cnt in per_kernel_all(d).items():
+            e = summary.setdefault(short(k), {"kernel": k, "avg_ns": dur.get(k)})
+            e.setdefault("sq", {}).update(cnt)
+    for e in summary.values():
+        sq = e.get("sq", {})
+        g, ns = sq.get("GRBM_GUI_ACTIVE"), e.get("avg_ns")
+        if g and ns:
+            e["clock_ghz"] = g / 8.0 / ns
+        if g and "SQ_VALU_MFMA_BUSY_CYCLES" in sq:
+            e["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 1024)
     with open(os.path.join(out, "%s_pmc_summary.json" % tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps({k: v for k, v in summary.items() if "policy_train" in k},
@@ -56,4 +80,4 @@ def main(tag, trace, fetch, write):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:])
