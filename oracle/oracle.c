@@ -323,27 +323,37 @@ int or_model_eval(const or_model *m, const float *params, const float *x,
  * matmul_layer::backward (nn.h:81-83): dX = bp A. */
 static void dense_grad(const float *A, int in, int out, const float *X,
                        const float *bp, size_t M, float *g, float *dX) {
+  /* row-major sweeps with double accumulators (the sums of nn.h:94-98 in
+   * row order; each entry rounded to float once) */
   float *dA = g, *db = g + (size_t)in * out;
-  for (int o = 0; o < out; ++o)
-    for (int k = 0; k < in; ++k) {
-      double s = 0.0;
-      for (size_t r = 0; r < M; ++r)
-        s += (double)bp[r * out + o] * (double)X[r * in + k];
-      dA[(size_t)o * in + k] = (float)s;
+  double *acc = (double *)calloc((size_t)in * out + out, sizeof(double));
+  double *accb = acc + (size_t)in * out;
+  for (size_t r = 0; r < M; ++r) {
+    const float *br = bp + r * out, *xr = X + r * in;
+    for (int o = 0; o < out; ++o) {
+      const double b = br[o];
+      double *ao = acc + (size_t)o * in;
+      for (int k = 0; k < in; ++k) ao[k] += b * (double)xr[k];
+      accb[o] += b;
     }
-  for (int o = 0; o < out; ++o) {
-    double s = 0.0;
-    for (size_t r = 0; r < M; ++r) s += (double)bp[r * out + o];
-    db[o] = (float)s;
   }
-  if (dX)
-    for (size_t r = 0; r < M; ++r)
-      for (int k = 0; k < in; ++k) {
-        double s = 0.0;
-        for (int o = 0; o < out; ++o)
-          s += (double)bp[r * out + o] * (double)A[(size_t)o * in + k];
-        dX[r * in + k] = (float)s;
+  for (size_t i = 0; i < (size_t)in * out; ++i) dA[i] = (float)acc[i];
+  for (int o = 0; o < out; ++o) db[o] = (float)accb[o];
+  free(acc);
+  if (dX) {
+    double *row = (double *)malloc(sizeof(double) * in);
+    for (size_t r = 0; r < M; ++r) {
+      for (int k = 0; k < in; ++k) row[k] = 0.0;
+      const float *br = bp + r * out;
+      for (int o = 0; o < out; ++o) {
+        const double b = br[o];
+        const float *ao = A + (size_t)o * in;
+        for (int k = 0; k < in; ++k) row[k] += b * (double)ao[k];
       }
+      for (int k = 0; k < in; ++k) dX[r * in + k] = (float)row[k];
+    }
+    free(row);
+  }
 }
 
 /* softmax_layer::backward (nn.h:393-417): recompute s, J = diag(s) - s s^T,
@@ -359,11 +369,68 @@ static void softmax_bwd_row(const float *z, const float *g, int n, float *out,
   for (int j = 0; j < n; ++j) out[j] = dotf(pd + (size_t)j * n, g, n);
 }
 
+/* Magnitude pass of one dense layer: the same sums over |terms| (the
+ * fp32-rounding scale of each gradient entry and of dX). */
+static void dense_grad_mag(const float *A, int in, int out, const float *X,
+                           const float *bpm, size_t M, float *gm, float *dXm) {
+  float *dA = gm, *db = gm + (size_t)in * out;
+  double *acc = (double *)calloc((size_t)in * out + out, sizeof(double));
+  double *accb = acc + (size_t)in * out;
+  for (size_t r = 0; r < M; ++r) {
+    const float *br = bpm + r * out, *xr = X + r * in;
+    for (int o = 0; o < out; ++o) {
+      const double b = br[o];
+      double *ao = acc + (size_t)o * in;
+      for (int k = 0; k < in; ++k) ao[k] += b * fabs((double)xr[k]);
+      accb[o] += b;
+    }
+  }
+  for (size_t i = 0; i < (size_t)in * out; ++i) dA[i] = (float)acc[i];
+  for (int o = 0; o < out; ++o) db[o] = (float)accb[o];
+  free(acc);
+  if (dXm) {
+    double *row = (double *)malloc(sizeof(double) * in);
+    for (size_t r = 0; r < M; ++r) {
+      for (int k = 0; k < in; ++k) row[k] = 0.0;
+      const float *br = bpm + r * out;
+      for (int o = 0; o < out; ++o) {
+        const double b = br[o];
+        const float *ao = A + (size_t)o * in;
+        for (int k = 0; k < in; ++k) row[k] += b * fabs((double)ao[k]);
+      }
+      for (int k = 0; k < in; ++k) dXm[r * in + k] = (float)row[k];
+    }
+    free(row);
+  }
+}
+
+static void or_model_grad_impl(const or_model *m, const float *params,
+                               const float *x, int rows, int xcols,
+                               or_loss_fn loss, void *ctx, float *grad,
+                               float *grad_mag);
+
 /* optimizer::step's forward + loss_grad + model::gradient (nn.h:594-605,
  * 481-488, 510-528).  Layer 0 only gets `gradient`, never `backward`. */
 void or_model_grad(const or_model *m, const float *params, const float *x,
                    int rows, int xcols, or_loss_fn loss, void *ctx,
                    float *grad) {
+  or_model_grad_impl(m, params, x, rows, xcols, loss, ctx, grad, NULL);
+}
+
+/* The same, plus grad_mag: for every gradient entry the sum over the
+ * magnitudes of the terms the reference's sums add up (|delta| propagated
+ * with |A|, |J| = diag(s) + s s^T for the softmax Jacobian), the scale of
+ * its fp32 rounding error under cancellation. */
+void or_model_grad_mag(const or_model *m, const float *params, const float *x,
+                       int rows, int xcols, or_loss_fn loss, void *ctx,
+                       float *grad, float *grad_mag) {
+  or_model_grad_impl(m, params, x, rows, xcols, loss, ctx, grad, grad_mag);
+}
+
+static void or_model_grad_impl(const or_model *m, const float *params,
+                               const float *x, int rows, int xcols,
+                               or_loss_fn loss, void *ctx, float *grad,
+                               float *grad_mag) {
   const int L = m->nl;
   float *acts[OR_MAX_LAYERS + 1];
   int cols[OR_MAX_LAYERS + 1];
@@ -379,43 +446,74 @@ void or_model_grad(const or_model *m, const float *params, const float *x,
   }
   float *bp = (float *)malloc(sizeof(float) * (size_t)rows * cols[L]);
   loss(ctx, acts[L], rows, cols[L], bp);
+  float *bpm = NULL; /* magnitudes of the incoming gradient terms */
+  if (grad_mag) {
+    bpm = (float *)malloc(sizeof(float) * (size_t)rows * cols[L]);
+    for (size_t i = 0; i < (size_t)rows * cols[L]; ++i) bpm[i] = fabsf(bp[i]);
+  }
   for (int l = L - 1; l >= 0; --l) {
     const int ic = cols[l], oc = cols[l + 1];
     const float *in = acts[l];
     float *nbp = l > 0 ? (float *)malloc(sizeof(float) * (size_t)rows * ic)
                        : NULL;
+    float *nbpm = (l > 0 && bpm)
+                      ? (float *)malloc(sizeof(float) * (size_t)rows * ic)
+                      : NULL;
     switch (m->type[l]) {
       case OR_FULL:
         dense_grad(params + poff[l], m->in[l], m->out[l], in, bp,
                    (size_t)rows, grad + poff[l], nbp);
+        if (bpm)
+          dense_grad_mag(params + poff[l], m->in[l], m->out[l], in, bpm,
+                         (size_t)rows, grad_mag + poff[l], nbpm);
         break;
       case OR_POINT: /* nn.h:149-186 reshaped to points */
         dense_grad(params + poff[l], m->in[l], m->out[l], in, bp,
                    (size_t)rows * (ic / m->in[l]), grad + poff[l], nbp);
+        if (bpm)
+          dense_grad_mag(params + poff[l], m->in[l], m->out[l], in, bpm,
+                         (size_t)rows * (ic / m->in[l]), grad_mag + poff[l],
+                         nbpm);
         break;
       case OR_RELU: /* nn.h:364-376: uses the layer input */
         if (nbp)
           for (size_t i = 0; i < (size_t)rows * ic; ++i)
             nbp[i] = in[i] > 0 ? bp[i] : 0;
+        if (nbpm)
+          for (size_t i = 0; i < (size_t)rows * ic; ++i)
+            nbpm[i] = in[i] > 0 ? bpm[i] : 0;
         break;
       case OR_SOFTMAX:
         if (nbp) {
           float *s = (float *)malloc(sizeof(float) * ic);
           float *pd = (float *)malloc(sizeof(float) * (size_t)ic * ic);
-          for (int r = 0; r < rows; ++r)
+          for (int r = 0; r < rows; ++r) {
             softmax_bwd_row(in + (size_t)r * ic, bp + (size_t)r * oc, ic,
                             nbp + (size_t)r * ic, s, pd);
+            if (nbpm) { /* |J| g_m = s * g_m + s (s . g_m) */
+              const float *gm = bpm + (size_t)r * oc;
+              double sg = 0.0;
+              for (int k = 0; k < ic; ++k) sg += (double)s[k] * gm[k];
+              for (int j = 0; j < ic; ++j)
+                nbpm[(size_t)r * ic + j] =
+                    (float)((double)s[j] * gm[j] + (double)s[j] * sg);
+            }
+          }
           free(s);
           free(pd);
         }
         break;
       case OR_SOFTMAX_XENT: /* nn.h:428-430: identity */
         if (nbp) memcpy(nbp, bp, sizeof(float) * (size_t)rows * ic);
+        if (nbpm) memcpy(nbpm, bpm, sizeof(float) * (size_t)rows * ic);
         break;
     }
     free(bp);
     bp = nbp;
+    free(bpm);
+    bpm = nbpm;
   }
+  free(bpm);
   for (int l = 1; l <= L; ++l) free(acts[l]);
 }
 
@@ -993,8 +1091,12 @@ void or_trainer_learn(or_trainer *t) {
     buf_set(&t->buf[OR_BUF_TARGETS], targets, rows, sizeof(float));
     float *vgrad = (float *)malloc(sizeof(float) * t->nv);
     sq_ctx sc = {targets};
-    or_model_grad(&t->val, t->vp, sm, rows, len, loss_square, &sc, vgrad);
+    float *vmag = (float *)malloc(sizeof(float) * t->nv);
+    or_model_grad_mag(&t->val, t->vp, sm, rows, len, loss_square, &sc, vgrad,
+                      vmag);
     buf_set(&t->buf[OR_BUF_VALUE_GRAD], vgrad, t->nv, sizeof(float));
+    buf_set(&t->buf[OR_BUF_VALUE_GRAD_MAG], vmag, t->nv, sizeof(float));
+    free(vmag);
     opt_step_scaled(t, &t->opt[1], t->vp, vgrad, t->nv);
     free(vgrad);
 
@@ -1067,16 +1169,22 @@ void or_trainer_learn(or_trainer *t) {
       pc.d_targ = t->d_targ;
     }
     buf_clear(&t->buf[OR_BUF_KL]);
+    buf_clear(&t->buf[OR_BUF_POLICY_GRADS_MAG]);
+    float *pmag = (float *)malloc(sizeof(float) * t->np);
     for (int e = 0; e < epochs; ++e) {
       const float beta_used = t->beta;
-      or_model_grad(&t->pol, t->pp, sm, rows, len, loss_policy, &pc, pgrad);
+      or_model_grad_mag(&t->pol, t->pp, sm, rows, len, loss_policy, &pc,
+                        pgrad, pmag);
       buf_append(&t->buf[OR_BUF_POLICY_GRADS], pgrad, t->np, sizeof(float));
+      buf_append(&t->buf[OR_BUF_POLICY_GRADS_MAG], pmag, t->np,
+                 sizeof(float));
       if (t->algo == OR_KLPPO) {
         const float kl[3] = {beta_used, (float)pc.d_avg, t->beta};
         buf_append(&t->buf[OR_BUF_KL], kl, 3, sizeof(float));
       }
       opt_step_scaled(t, &t->opt[0], t->pp, pgrad, t->np);
     }
+    free(pmag);
   }
   buf_set(&t->buf[OR_BUF_ADVANTAGES], adv, rows, sizeof(float));
   free(adv);

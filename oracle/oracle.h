@@ -83,6 +83,9 @@ typedef void (*or_loss_fn)(void *ctx, const float *out, int rows, int cols,
 void or_model_grad(const or_model *m, const float *params, const float *x,
                    int rows, int xcols, or_loss_fn loss, void *ctx,
                    float *grad);
+void or_model_grad_mag(const or_model *m, const float *params, const float *x,
+                       int rows, int xcols, or_loss_fn loss, void *ctx,
+                       float *grad, float *grad_mag);
 void or_sgd(float *params, const float *grad, size_t n, float lr, float wd);
 /* sgd / momentum / adam optimizers (nn.h:616-698) with their state. */
 enum { OR_OPT_SGD = 0, OR_OPT_MOMENTUM = 1, OR_OPT_ADAM = 2 };
@@ -152,6 +155,10 @@ enum {
   OR_BUF_ROW_POLD,      /* float  [rows]  distrib[choice] of the row       */
   OR_BUF_KL,            /* float  [epochs][3] KL-PPO: beta used, mean KL,
                                               beta after                   */
+  OR_BUF_POLICY_GRADS_MAG, /* float [epochs][policy params]: per entry, the
+                              sum of |terms| of its row sums (rounding
+                              scale, or_model_grad_mag) -- AC / PPO / KL   */
+  OR_BUF_VALUE_GRAD_MAG,   /* float [value params]: the same              */
   OR_BUF_COUNT
 };
 /* Returns a pointer to the buffer and its element count. */

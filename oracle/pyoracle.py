@@ -18,7 +18,8 @@ OPT_SGD, OPT_MOMENTUM, OPT_ADAM = range(3)
 (BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE, BUF_STEP_PCHOICE,
  BUF_ROWS, BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_VALUES, BUF_TARGETS,
  BUF_VALUE_GRAD, BUF_ADVANTAGES, BUF_POLICY_GRADS, BUF_FINAL_BINS,
- BUF_FINAL_ITEM, BUF_ROW_CHOICE, BUF_ROW_POLD, BUF_KL) = range(19)
+ BUF_FINAL_ITEM, BUF_ROW_CHOICE, BUF_ROW_POLD, BUF_KL, BUF_POLICY_GRADS_MAG,
+ BUF_VALUE_GRAD_MAG) = range(21)
 _INT_BUFS = {BUF_STEP_BINS, BUF_STEP_ITEM, BUF_STEP_CHOICE, BUF_STEP_DONE,
              BUF_ROW_ENV, BUF_ROW_STEP, BUF_ROW_IS_END, BUF_FINAL_BINS,
              BUF_FINAL_ITEM, BUF_ROW_CHOICE}

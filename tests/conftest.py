@@ -37,6 +37,33 @@ def assert_close(x, y, tol=RTOL, what=""):
     return float(err.max()) if err.size else 0.0
 
 
+# Row-summed gradients under cancellation.  A gradient entry is a sum over
+# the batch rows (nn.h:94-98), and a policy-gradient entry cancels heavily
+# (softmax Jacobian rows sum to zero), so |sum| can be ~1e-3 of the sum of
+# |terms|.  Any fp32 evaluation order of n terms is within (n - 1) u
+# sum|terms| of the exact sum (recursive-summation bound; + u per product for
+# the terms' own rounding), u = 2^-24.  The oracle accumulates in double
+# (sides = 1); the reference's own fp32 sums carry the same bound again
+# (sides = 2).  Rule: |x - y| <= 1e-4 max(1, |y|) + sides (n + 8) u mag, with
+# mag = sum|terms| per entry from or_model_grad_mag.
+U32 = 2.0 ** -24
+
+
+def assert_grad_close(x, y, mag, n_terms, sides=1, what=""):
+    x = np.asarray(x, np.float64).ravel()
+    y = np.asarray(y, np.float64).ravel()
+    mag = np.asarray(mag, np.float64).ravel()
+    assert x.shape == y.shape == mag.shape, (what, x.shape, y.shape, mag.shape)
+    bound = RTOL * np.maximum(1.0, np.abs(y)) + sides * (n_terms + 8) * U32 * mag
+    err = np.abs(x - y)
+    if err.size:
+        i = int(np.argmax(err / bound))
+        assert err[i] <= bound[i], (
+            "%s: err %.3g > bound %.3g at %d (x=%r y=%r mag=%.3g)" % (
+                what, err[i], bound[i], i, x[i], y[i], mag[i]))
+    return float((err / bound).max()) if err.size else 0.0
+
+
 # adam_optimizer (nn.h:677-690) divides each gradient entry by its own running
 # RMS, so an entry whose gradient is fp32 rounding noise (a sum that cancels to
 # ~1e-7 of the gradient's largest entry) takes a step of up to lr with an

@@ -70,6 +70,11 @@ FIXTURES = {
     # BASELINE config 3/4 shape (2-D, 64 bins, [128,128])
     "ppo_b64d2": ("learn", ["algo=ppo", "B=64", "D=2", "widths=128,128",
                             "N=4", "T=4", "iters=2", "seed=11"]),
+    # the config-3 shape with enough envs for several 64-row groups per train
+    # workgroup (640 groups per epoch): the device's multi-group dW
+    # accumulation pinned by the reference itself, not only by the oracle
+    "ppo_b64d2_n160": ("learn", ["algo=ppo", "B=64", "D=2", "widths=128,128",
+                                 "N=160", "T=4", "iters=2", "seed=31"]),
     # ppo2_training.cc: KL-regulated PPO, conv 4->128->64->1 + softmax,
     # policy sgd(1e-4, wd 1e-5), 16 workers x 8 steps; beta carries over
     "klppo_b8d2": ("learn", ["algo=klppo", "B=8", "D=2", "widths=128,64",

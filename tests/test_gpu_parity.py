@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 
 
 
-ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3",
+ENV_CASES = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ppo_b64d2_n160", "ac_b8d2",
+             "ac_b128d3",
              "klppo_b8d2"]
 
 
@@ -91,7 +92,7 @@ def test_rollout_sampling_matches_reference(ctx, name):
 
 @pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2",
                                   "ac_b128d3", "klppo_b8d2", "ppo_adam_b8d2",
-                                  "ac_mom_b8d2"])
+                                  "ac_mom_b8d2", "ppo_b64d2_n160"])
 def test_learn_matches_reference(ctx, name):
     """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
     value gradient and updated parameters vs the reference learner (sgd, and

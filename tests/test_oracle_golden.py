@@ -104,7 +104,8 @@ def test_weights20_logits_and_argmax_episodes():
 
 # ------------------------------------------------------------- learners ----
 LEARN = ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2", "ac_b128d3", "pg_b8d1",
-         "klppo_b8d2", "ppo_adam_b8d2", "ac_mom_b8d2", "pg_b8d2"]
+         "klppo_b8d2", "ppo_adam_b8d2", "ac_mom_b8d2", "pg_b8d2",
+         "ppo_b64d2_n160"]
 ALGO = {"ppo": po.OR_PPO, "ac": po.OR_AC, "pg": po.OR_PG, "klppo": po.OR_KLPPO}
 OPT = {"sgd": po.OPT_SGD, "momentum": po.OPT_MOMENTUM, "adam": po.OPT_ADAM}
 
