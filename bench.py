@@ -69,28 +69,64 @@ def value_fwd_flops_per_row():
     return 2 * (fin * V1 + V1 * V2 + V2)
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """Time the reference's single-threaded CPU path on a bounded sample of
-    the same workload (64 bins, 2-D, [128,128], PPO k=4, T=4)."""
+def _harness_cmd(harness, n_env, iters, seed):
+    return [harness, "bench", "algo=%s" % ALGO, "B=%d" % B, "D=%d" % D,
+            "widths=%d,%d" % (H1, H2), "N=%d" % n_env, "T=%d" % T,
+            "iters=%d" % iters, "seed=%d" % seed]
+
+
+def host_cores():
+    """CPU cores this process may use, capped at the GPU box's per-GPU share
+    (16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline():
+    """Time the reference's single-threaded CPU path (oracle/_ref/ref_harness
+    = the reference's own ppo_learner / actor_critic_learner and agents,
+    compiled from its sources) on a bounded sample of the same workload:
+    first one process alone (the single-core rate), then one independent
+    seeded process per usable core at once (the whole-host rate, SURVEY
+    8(d): the reference path is single-threaded, so a whole host runs it as
+    that many independent processes).  About 2 x 8 s."""
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    n_env, iters = 16, REF_ITERS  # 10-20 s on one core
+    n_env, iters = 16, max(1, REF_ITERS // 3)
     learner = "ppo_learner" if ALGO == "ppo" else "actor_critic_learner"
-    sample = ("reference %s, %d envs x T=%d x %d iterations, B=%d D=%d "
-              "[%d,%d], 1 thread" % (learner, n_env, T, iters, B, D, H1, H2))
+    sample = ("reference %s, %d envs x T=%d x %d iterations per process, "
+              "B=%d D=%d [%d,%d], single-threaded processes" % (
+                  learner, n_env, T, iters, B, D, H1, H2))
     if os.path.exists(harness):
         try:
-            out = subprocess.run(
-                [harness, "bench", "algo=%s" % ALGO, "B=%d" % B, "D=%d" % D,
-                 "widths=%d,%d" % (H1, H2),
-                 "N=%d" % n_env, "T=%d" % T, "iters=%d" % iters, "seed=1"],
-                capture_output=True, text=True, timeout=600, check=True)
-            r = json.loads(out.stdout.strip().splitlines()[-1])
-            return {"value": round(r["env_steps_per_s"], 3),
-                    "unit": "env-steps/s", "cores": 1, "kind": "reference",
-                    "sample": sample}
+            out = subprocess.run(_harness_cmd(harness, n_env, iters, 1),
+                                 capture_output=True, text=True, timeout=600,
+                                 check=True)
+            single = json.loads(out.stdout.strip().splitlines()[-1])
+            cores = host_cores()
+            procs = [subprocess.Popen(_harness_cmd(harness, n_env, iters, 1 + k),
+                                      stdout=subprocess.PIPE, text=True)
+                     for k in range(cores)]
+            rates = []
+            for p in procs:
+                o, _ = p.communicate(timeout=600)
+                if p.returncode != 0:
+                    raise RuntimeError("harness rc %d" % p.returncode)
+                rates.append(json.loads(o.strip().splitlines()[-1])["env_steps_per_s"])
+            return {"value": round(sum(rates), 3), "unit": "env-steps/s",
+                    "cores": cores, "kind": "reference",
+                    "sample": sample + "; value = sum over %d concurrent "
+                              "processes" % cores,
+                    "single_core": round(single["env_steps_per_s"], 3),
+                    "per_process_min": round(min(rates), 3)}
         except Exception as e:  # fall through to the port
             print("cpu_baseline: reference harness failed: %s" % e,
                   file=sys.stderr)
+    # the reference harness is built from /root/reference in the build
+    # container; without it, the oracle port (the reference's loop structure
+    # restated in C) is timed instead and `kind` says so
     from oracle import pyoracle as po
     from dependence_free_rl_amd.trainer import init_policy, init_value
     n_env, iters = 8, 3
@@ -144,9 +180,15 @@ def main():
                     help="BASELINE.json config (3 = the headline)")
     ap.add_argument("--envs", type=int, default=None,
                     help="envs per GPU (default: the config's)")
+    ap.add_argument("--rollout-steps", type=int, default=None,
+                    help="T, env steps per env per iteration (default: the "
+                         "config's; SURVEY 8(d)'s larger-T throughput point)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     cfg = select_config(args.config)
+    if args.rollout_steps:
+        global T
+        T = args.rollout_steps
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +212,7 @@ def main():
         uid = rdzv.broadcast(Context.unique_id() if rank == 0 else None)
 
     from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
-                                        init_policy, init_value)
+                                        init_policy, init_value, runtime_info)
     ctx = Context(device=device, rank=rank, world=world, uid=uid)
     n = args.envs or cfg["N"]
     tr = Trainer(ctx, algo=ALGO, bins=B, dims=D, num_envs=n, steps=T,
@@ -196,6 +238,9 @@ def main():
     if rdzv:
         dt = rdzv.allreduce_max(dt)
 
+    # numerical health of what was timed (after the timed region): finite
+    # parameters / probabilities, done rate and mean episode length
+    health = tr.health()
     ms_pt, n_pt = tr.kernel_time("policy_train")
     ms_ro, n_ro = tr.kernel_time("rollout_step")
     ms_v, _ = tr.kernel_time("value")
@@ -242,7 +287,9 @@ def main():
         "dtype": "f32",
         "data": "synthetic (fixed-size bin-packing instances, random-init "
                 "weights of the reference architecture)",
-        "config": {"workload": workload + cfg["name"] % n,
+        "config": {"workload": workload + cfg["name"] % n + (
+                       "; larger-T point: T=%d" % T if args.rollout_steps
+                       else ""),
                    "envs_per_gpu": n, "bins": B, "dims": D, "T": T,
                    "epochs": EPOCHS, "parallelism": "dp%d" % world},
         "roofline": {"kernel": "policy_train", "bound": "mfma",
@@ -260,6 +307,8 @@ def main():
                          "achieved": round(hbm_gbs, 2),
                          "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                          "frac": round(hbm_gbs / (HBM_PEAK_GBS * world), 6)},
+        "health": health,
+        "runtime": runtime_info(),
         "phase_ms_per_step": {
             "rollout": round(ms_ro / args.steps, 3),
             "policy_train": round(ms_pt / args.steps, 3),

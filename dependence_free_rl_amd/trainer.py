@@ -308,6 +308,23 @@ class Trainer:
         check(_lib.lib.xh_trainer_set_env_state(self.h, first, count,
                                                 _ptr(bins), _ptr(items)))
 
+    def health(self):
+        """Numerical health of the training state (host copies, call outside
+        any timed region): finite parameters and last-step probabilities,
+        and the last batch's done rate / mean episode length (every episode
+        ends on exactly one done step)."""
+        pp, pv = self.params(POLICY), self.params(VALUE)
+        out = {"finite": bool(np.isfinite(pp).all() and np.isfinite(pv).all())}
+        if self.cfg.algo != XH_PG:
+            probs = self.buffer(BUF_PROBS)
+            done = self.buffer(BUF_DONE)
+            out["finite"] = out["finite"] and bool(np.isfinite(probs).all())
+            out["max_prob"] = float(probs.max())
+            rate = float(done.mean())
+            out["done_rate"] = rate
+            out["mean_episode_len"] = (1.0 / rate) if rate > 0 else None
+        return out
+
     def evaluate(self, n_envs, episodes, rng_state, argmax_probs=False,
                  init_items=None, trace_cap=0):
         """Argmax evaluation (deep_agent.cc / the drivers' periodic eval).

@@ -262,3 +262,27 @@ def test_bench_json_line(tmp_path):
     assert abs(d["value"] * d["ms_per_step"] / 1e3 - 256 * 4) < 1e-3 * 256 * 4 + 1
     r = d["roofline"]
     assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and r["peak"] == 157.3
+
+
+def test_c3_numerics_over_bench_length(ctx):
+    """The bench workload (BASELINE config 3, reference lrs on row SUMS with
+    no max-shift softmax) stays numerically healthy over 25 iterations:
+    finite parameters, probabilities and advantages after every 5; the mean
+    episode length is logged (and must be a real number of steps)."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import BUF_ADV
+    N, B, D, T = 32768, 64, 2, 4
+    tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
+                 rng_state=20241008)
+    tr.set_params(POLICY, init_policy(D, 128, 128, seed=0))
+    tr.set_params(VALUE, init_value(B, D, seed=1))
+    log = []
+    for k in range(5):
+        tr.iterate(5)
+        h = tr.health()
+        log.append((5 * (k + 1), round(h["mean_episode_len"], 2),
+                    round(h["max_prob"], 4)))
+        assert h["finite"], (k, h)
+        assert np.isfinite(tr.buffer(BUF_ADV)).all()
+        assert 1.0 <= h["mean_episode_len"] <= B * 8 * D + 1, h
+    print("iteration, mean episode length, max prob:", log)
