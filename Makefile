@@ -57,13 +57,21 @@ oracle:
 	$(MAKE) -C oracle port
 	@if [ -d /root/reference ]; then $(MAKE) -C oracle ref; fi
 
-compat: $(EXAMPLES)
+# test programs of the drop-in layer (tests/compat), prebuilt so the GPU box
+# runs them without a compiler step
+COMPAT_TESTS := $(COMPAT)/bound_env_by_hand
+
+compat: $(EXAMPLES) $(COMPAT_TESTS)
 	@mkdir -p $(COMPAT)
 	@if [ -d $(REF)/apps/bin_packing ]; then \
 	  for a in $(REF_APPS); do \
 	    $(CXX20) $(CXXFLAGS20) -Wno-logical-op-parentheses \
 	      $(REF)/apps/bin_packing/$$a.cc $(LDCOMPAT) -o $(COMPAT)/$$a || exit 1; \
 	  done; fi
+
+$(COMPAT)/bound_env_by_hand: tests/compat/bound_env_by_hand.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
 
 $(COMPAT)/%: examples/%.cc $(COMPAT_HDRS) $(LIB)
 	@mkdir -p $(COMPAT)

@@ -108,6 +108,8 @@ def _load():
         "xh_venv_reset": (i, [vp, i]),
         "xh_venv_observe": (i, [vp]),
         "xh_venv_synchronize": (i, [vp]),
+        "xh_model_eval": (i, [vp, vp, i, vp, sz, vp, i, i, vp, sz,
+                              C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -116,8 +118,16 @@ def _load():
     return lib
 
 
+class Layer(C.Structure):
+    """Mirror of xh_layer."""
+    _fields_ = [("kind", C.c_int), ("inp", C.c_int), ("out", C.c_int)]
+
+
+LAYER_FULL, LAYER_CONV1D_1, LAYER_RELU, LAYER_SOFTMAX, LAYER_SOFTMAX_XENT = range(5)
+
 lib = _load()
-for _name, _mirror in (("xh_config", Config), ("xh_eval", Eval)):
+for _name, _mirror in (("xh_config", Config), ("xh_eval", Eval),
+                       ("xh_layer", Layer)):
     if lib.xh_struct_size(_name.encode()) != C.sizeof(_mirror):
         raise ImportError("ctypes mirror of %s is out of date (%d vs %d bytes)"
                           % (_name, C.sizeof(_mirror),

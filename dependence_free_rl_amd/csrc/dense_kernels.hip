@@ -324,4 +324,79 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
   return e;
 }
 
+// ------------------------------------------------ model::eval on device --
+// softmax_layer / softmax_cross_entropy_layer forward (nn.h:382-392, 424-431):
+// exp(z) / sum exp(z) over each row, no max shift, the sum in column order.
+__global__ void softmax_rows_kernel(float *y, int rows, int cols) {
+#pragma clang fp contract(off)
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += gridDim.x * blockDim.x) {
+    float *row = y + (size_t)r * cols;
+    float sum = 0.0f;
+    for (int c = 0; c < cols; ++c) {
+      row[c] = expf(row[c]);
+      sum += row[c];
+    }
+    for (int c = 0; c < cols; ++c) row[c] = row[c] / sum;
+  }
+}
+
+__global__ void relu_kernel(float *y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = y[i] > 0.0f ? y[i] : 0.0f;
+}
+
+// Forward of a layer chain over `rows` input rows of `cols` features (every
+// buffer device memory; a and b are ping-pong buffers big enough for the
+// widest activation).  Dense layers run on the f32 MFMA GEMM with the bias
+// and a following relu fused into the epilogue; conv1d_1 is the same GEMM
+// over rows * (cols / in) points (nn.h:127-147).  Returns the output's
+// buffer and column count.
+hipError_t model_forward(const ModelLayer *layers, int nl, const float *params,
+                         const float *x, int rows, int cols, float *a, float *b,
+                         const float **out, int *out_cols, hipStream_t s) {
+  using namespace dense;
+  const float *cur = x;
+  float *bufs[2] = {a, b};
+  int which = 0;
+  size_t poff = 0;
+  hipError_t e = hipSuccess;
+  for (int l = 0; l < nl && e == hipSuccess; ++l) {
+    const ModelLayer &L = layers[l];
+    float *dst = bufs[which];
+    if (L.kind == kLayerFull || L.kind == kLayerConv1d) {
+      const int pts = L.kind == kLayerFull ? 1 : cols / L.in;
+      const int M = rows * pts;
+      const float *W = params + poff;
+      const bool fuse = l + 1 < nl && layers[l + 1].kind == kLayerRelu;
+      EpBiasAct ep{dst, L.out, W + (size_t)L.out * L.in, fuse ? 1 : 0};
+      RowMajor la{cur, L.in};
+      RowMajor wt{W, L.in};
+      e = gemm(la, wt, ep, M, L.out, L.in, nullptr, 0, 1, s);
+      poff += (size_t)L.out * L.in + L.out;
+      cols = pts * L.out;
+      if (fuse) ++l;
+    } else {
+      const long n = (long)rows * cols;
+      if (cur != dst)
+        e = hipMemcpyAsync(dst, cur, n * 4, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) {
+        if (L.kind == kLayerRelu)
+          hipLaunchKernelGGL(relu_kernel, dim3((unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096)),
+                             dim3(256), 0, s, dst, n);
+        else
+          hipLaunchKernelGGL(softmax_rows_kernel, dim3((rows + 255) / 256),
+                             dim3(256), 0, s, dst, rows, cols);
+        e = hipGetLastError();
+      }
+    }
+    cur = dst;
+    which ^= 1;
+  }
+  *out = cur;
+  *out_cols = cols;
+  return e;
+}
+
 }  // namespace xh

@@ -176,6 +176,16 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s);
 hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
                         hipStream_t s);
 
+// model::eval of a described layer chain (dense_kernels.hip, xh_model_eval).
+enum LayerKind { kLayerFull = 0, kLayerConv1d = 1, kLayerRelu = 2,
+                 kLayerSoftmax = 3, kLayerSoftmaxXent = 4 };
+struct ModelLayer {
+  int kind, in, out;
+};
+hipError_t model_forward(const ModelLayer *layers, int nl, const float *params,
+                         const float *x, int rows, int cols, float *a, float *b,
+                         const float **out, int *out_cols, hipStream_t s);
+
 // REINFORCE (pg_kernels.hip).  Batch.T = the per-iteration step bound.
 struct PgStepArgs {
   EnvDesc env;

@@ -944,6 +944,7 @@ size_t xh_struct_size(const char *name) {
   if (!name) return 0;
   if (!std::strcmp(name, "xh_config")) return sizeof(xh_config);
   if (!std::strcmp(name, "xh_eval")) return sizeof(xh_eval);
+  if (!std::strcmp(name, "xh_layer")) return sizeof(xh_layer);
   return 0;
 }
 
@@ -1577,6 +1578,73 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
       t->env_override[first + e] = std::move(v);
     }
     return XH_OK;
+  });
+}
+
+// ---------------------------------------------------------- model::eval --
+int xh_model_eval(xh_ctx *ctx, const xh_layer *layers, int nlayers,
+                  const float *params, size_t nparams, const float *x,
+                  int rows, int cols, float *out, size_t out_cap,
+                  int *out_cols) {
+  return guard([&]() -> int {
+    if (!ctx || !layers || nlayers < 1 || !params || !x || !out || !out_cols)
+      return fail(XH_ERR_INVALID, "model_eval: null arg");
+    if (rows < 1 || cols < 1)
+      return fail(XH_ERR_INVALID, "model_eval: %d x %d input", rows, cols);
+    std::vector<xh::ModelLayer> ml((size_t)nlayers);
+    size_t np = 0, widest = (size_t)cols;
+    int c = cols;
+    for (int l = 0; l < nlayers; ++l) {
+      const xh_layer &L = layers[l];
+      ml[l] = xh::ModelLayer{L.kind, L.in, L.out};
+      switch (L.kind) {
+        case XH_LAYER_FULL:
+        case XH_LAYER_CONV1D_1:
+          if (L.in < 1 || L.out < 1 ||
+              (L.kind == XH_LAYER_FULL ? c != L.in : c % L.in != 0))
+            return fail(XH_ERR_INVALID, "model_eval: layer %d (%d -> %d) on "
+                        "%d features", l, L.in, L.out, c);
+          c = L.kind == XH_LAYER_FULL ? L.out : c / L.in * L.out;
+          np += (size_t)L.out * L.in + L.out;
+          break;
+        case XH_LAYER_RELU:
+        case XH_LAYER_SOFTMAX:
+        case XH_LAYER_SOFTMAX_XENT:
+          break;
+        default:
+          return fail(XH_ERR_INVALID, "model_eval: layer kind %d", L.kind);
+      }
+      widest = std::max(widest, (size_t)c);
+    }
+    if (np != nparams)
+      return fail(XH_ERR_INVALID, "model_eval: %zu parameters, the layers "
+                  "need %zu", nparams, np);
+    if ((size_t)rows * c > out_cap)
+      return fail(XH_ERR_INVALID, "model_eval: output needs %zu floats, "
+                  "capacity %zu", (size_t)rows * c, out_cap);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t act = (size_t)rows * widest;
+    float *dev = nullptr;
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMalloc((void **)&dev, sizeof(float) * (np + 3 * act)));
+    float *dp = dev, *dx = dev + np, *da = dx + act, *db = da + act;
+    int st = copy_ok(copy_to_device(dp, params, np * 4, s));
+    if (st == XH_OK)
+      st = copy_ok(copy_to_device(dx, x, (size_t)rows * cols * 4, s));
+    const float *res = nullptr;
+    int oc = 0;
+    if (st == XH_OK) {
+      const hipError_t e = xh::model_forward(ml.data(), nlayers, dp, dx, rows,
+                                             cols, da, db, &res, &oc, s);
+      if (e != hipSuccess)
+        st = fail(XH_ERR_HIP, "model_eval: %s", hipGetErrorString(e));
+    }
+    if (st == XH_OK) st = copy_ok(copy_to_host(out, res, (size_t)rows * oc * 4, s));
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(dev);
+    if (st == XH_OK) *out_cols = oc;
+    return st;
   });
 }
 

@@ -116,6 +116,29 @@ def heuristic_evaluate(ctx, kind, bins, dims, n_envs, episodes, rng_state,
     return _eval_result(e, out, trace_cap)
 
 
+def model_eval(ctx, layers, params, x):
+    """xylo::model::eval on the device (xh_model_eval).  layers: sequence of
+    (kind, in, out) with kind in "full" | "conv1d_1" | "relu" | "softmax" |
+    "softmax_xent" (in / out ignored for the activations); x: [rows][cols]."""
+    kinds = {"full": _lib.LAYER_FULL, "conv1d_1": _lib.LAYER_CONV1D_1,
+             "relu": _lib.LAYER_RELU, "softmax": _lib.LAYER_SOFTMAX,
+             "softmax_xent": _lib.LAYER_SOFTMAX_XENT}
+    arr = (_lib.Layer * len(layers))()
+    for i, (k, a, b) in enumerate(layers):
+        arr[i].kind, arr[i].inp, arr[i].out = kinds[k], a, b
+    x = np.ascontiguousarray(x, np.float32)
+    p = np.ascontiguousarray(params, np.float32)
+    rows, cols = x.shape
+    widest = max([cols] + [b * (cols // a if k == "conv1d_1" else 1)
+                           for k, a, b in layers if k in ("full", "conv1d_1")])
+    out = np.zeros(rows * widest, np.float32)
+    oc = C.c_int()
+    check(_lib.lib.xh_model_eval(ctx.h, arr, len(layers), _ptr(p), p.size,
+                                 _ptr(x), rows, cols, _ptr(out), out.size,
+                                 C.byref(oc)))
+    return out[:rows * oc.value].reshape(rows, oc.value).copy()
+
+
 def policy_param_count(dims, h1, h2):
     f0 = 2 * dims
     return h1 * f0 + h1 + h2 * h1 + h2 + h2 + 1

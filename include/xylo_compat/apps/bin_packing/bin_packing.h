@@ -100,21 +100,27 @@ class environment : public xylo::environment<action, observation> {
   environment(const environment &) = delete;
   ~environment() override;
 
-  // bin_packing.h:53-64
+  // bin_packing.h:53-64.  A device-bound env's state lives in the trainer's
+  // HBM buffers: it is viewed from there, changed here with the same engine
+  // draws, and written back as the state its next rollout starts from.
   void apply(const action &a, std::size_t) override {
-    host_only("apply");
-    std::pair<int, int> &bin = state_.bins[a.choice];
-    bin.first -= state_.item.first;
-    bin.second -= state_.item.second;
-    if (bin.first < 0 || bin.second < 0) return;
-    get_item();
+    if (bound_) {
+      observation s = view(0);
+      apply_to(s, a);
+      bound_write(s);
+      return;
+    }
+    apply_to(state_, a);
   }
   observation view(std::size_t) const override;
   // bin_packing.h:67-70
   void reset(std::size_t) override {
-    host_only("reset");
-    state_ = observation(capacity);
-    get_item();
+    observation s(capacity);
+    s.item = draw_item();
+    if (bound_)
+      bound_write(s);
+    else
+      state_ = std::move(s);
   }
 
   // ---- device binding ----------------------------------------------------
@@ -127,15 +133,19 @@ class environment : public xylo::environment<action, observation> {
   int bound_index() const { return index_; }
 
  private:
-  void host_only(const char *what) const {
-    if (bound_)
-      throw xeno::error(std::string("bp::environment::") + what +
-                        " on an env whose state lives on the device");
+  void apply_to(observation &s, const action &a) {
+    std::pair<int, int> &bin = s.bins[a.choice];
+    bin.first -= s.item.first;
+    bin.second -= s.item.second;
+    if (bin.first < 0 || bin.second < 0) return;
+    s.item = draw_item();
   }
+  void bound_write(const observation &s);  // bin_packing_device.h
   // bin_packing.h:76-81: 2 engine draws (generate_canonical<double>).
-  void get_item() {
-    state_.item = dist_(xylo::default_generator()) ? shape1 : shape2;
+  std::pair<int, int> draw_item() {
+    return dist_(xylo::default_generator()) ? shape1 : shape2;
   }
+  void get_item() { state_.item = draw_item(); }
 
   observation state_;
   std::bernoulli_distribution dist_;

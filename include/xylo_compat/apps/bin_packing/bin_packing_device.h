@@ -30,20 +30,8 @@ inline std::uint32_t minstd_jump(std::uint32_t x, std::uint64_t n) {
   return std::uint32_t(r * x % m);
 }
 
-// ---- the process-wide device context -----------------------------------
-inline xh_ctx *context() {
-  struct holder {
-    xh_ctx *h = nullptr;
-    holder() {
-      const char *d = std::getenv("XYLO_HIP_DEVICE");
-      check(xh_ctx_create(d ? std::atoi(d) : 0, 0, 1, nullptr, &h),
-            "xh_ctx_create");
-    }
-    ~holder() { xh_ctx_destroy(h); }
-  };
-  static holder c;
-  return c.h;
-}
+// ---- the process-wide device context (xylo/nn.h) ------------------------
+inline xh_ctx *context() { return xylo::detail::hip_context(); }
 
 struct trainer {
   xh_trainer *h = nullptr;
@@ -373,9 +361,32 @@ class session {
     return o;
   }
 
+  // env.apply / env.reset of a device-bound env by host code: the new state
+  // is what that env's next rollout starts from (xh_trainer_set_env_state);
+  // the current window's trajectories are untouched.
+  void set_env_state(int index, const observation &o) {
+    flush_all();
+    if (pg())
+      throw xeno::error("xylo-hip: host apply / reset of an env bound to a "
+                        "REINFORCE window is not supported");
+    const int B = int(num_bins);
+    std::vector<std::int8_t> b(std::size_t(B) * 2), it(2);
+    for (int i = 0; i < B; ++i) {
+      b[2 * i] = std::int8_t(o.bins[i].first);
+      b[2 * i + 1] = std::int8_t(o.bins[i].second);
+    }
+    it[0] = std::int8_t(o.item.first);
+    it[1] = std::int8_t(o.item.second);
+    check(xh_trainer_set_env_state(tr_->h, index, 1, b.data(), it.data()),
+          "xh_trainer_set_env_state");
+    overrides_[index] = o;
+  }
+
   // env.view() of a device-bound env: its current state on the device.
   observation device_view(int index) {
     flush_all();
+    auto ov = overrides_.find(index);
+    if (ov != overrides_.end()) return ov->second;
     const int N = int(envs_.size()), B = int(num_bins);
     std::vector<std::int8_t> bins(std::size_t(T_ + 1) * N * B * 2),
         items(std::size_t(T_ + 1) * N * 4);
@@ -602,6 +613,7 @@ class session {
     check(xh_trainer_seed_streams(tr_->h, x), "xh_trainer_seed_streams");
     eng.seed(minstd_jump(x, 4ull * T_ * envs_.size()));
     check(xh_trainer_rollout(tr_->h), "xh_trainer_rollout");
+    overrides_.clear();  // the rollout started from them
     state_ = rolled;
     materialised_ = false;
     slot_ = T_;
@@ -758,6 +770,7 @@ class session {
   long steps_ = 0;
   std::uint32_t x_first_ = 0;
   std::uint64_t pol_version_ = ~0ull, val_version_ = ~0ull;
+  std::map<int, observation> overrides_;  // host apply / reset since the roll
 };
 
 inline void flush_all() {
@@ -793,6 +806,10 @@ inline environment::~environment() {
 inline observation environment::view(std::size_t) const {
   if (bound_) return bound_->device_view(index_);
   return state_;
+}
+
+inline void environment::bound_write(const observation &s) {
+  bound_->set_env_state(index_, s);
 }
 
 }  // namespace bp
@@ -834,11 +851,17 @@ template <> struct device_traits<bp::action, bp::observation> {
         .request_episodes(a, *env, p->device_model(), k);
     return true;
   }
+  // A host-policy step of a device-bound env goes through the env's device
+  // view / apply / reset; only recording it into the replay buffer whose
+  // device window that env belongs to is refused (the window's trajectories
+  // are the device's).
   static void before_host_step(agent<A, S> &a) {
     bp::device::flush_all();
     if (auto *env = dynamic_cast<bp::environment *>(&a.bound_env()))
-      if (env->bound_session())
-        throw xeno::error("xylo-hip: host step on a device-bound env");
+      if (env->bound_session() &&
+          a.bound_buffer().device_state().get() == env->bound_session())
+        throw xeno::error("xylo-hip: host step of a device-bound env into "
+                          "its own device window's replay buffer");
   }
   static void materialise(replay_buffer<A, S> &rb) {
     if (rb.device_state()) bp::device::session_of(rb).materialise(rb);

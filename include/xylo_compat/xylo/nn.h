@@ -8,12 +8,15 @@
 // global engine with the reference's schemes, so a seeded run starts from the
 // reference's weights.  The arithmetic (eval / forward / gradient / optimizer
 // step) is not on the host: a model is executed by the HIP kernels of
-// include/xylo_hip.h when a device learner or policy uses it, and the device
-// copy of the parameters is pulled back lazily by parameters().
+// include/xylo_hip.h when a device learner or policy uses it (model::eval
+// through xh_model_eval), and the device copy of the parameters is pulled
+// back lazily by parameters().
 #ifndef XYLO_HIP_COMPAT_NN_H_
 #define XYLO_HIP_COMPAT_NN_H_
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <fstream>
 #include <functional>
@@ -27,8 +30,27 @@
 #include <xeno/logging.h>
 #include <xeno/string.h>
 #include <xylo/tensor.h>
+#include <xylo_hip.h>
 
 namespace xylo {
+
+namespace detail {
+// The process-wide device context (XYLO_HIP_DEVICE picks the GPU).
+inline xh_ctx *hip_context() {
+  struct holder {
+    xh_ctx *h = nullptr;
+    holder() {
+      const char *d = std::getenv("XYLO_HIP_DEVICE");
+      if (xh_ctx_create(d ? std::atoi(d) : 0, 0, 1, nullptr, &h) != XH_OK)
+        throw xeno::error(std::string("xylo-hip: xh_ctx_create: ") +
+                          xh_last_error());
+    }
+    ~holder() { xh_ctx_destroy(h); }
+  };
+  static holder c;
+  return c.h;
+}
+}  // namespace detail
 
 inline void normal_initialize(std::size_t, vector_view v) {
   normal_distribution(0, 0.01, v);
@@ -160,10 +182,48 @@ class model {
     ++host_version_;
   }
 
-  // No host arithmetic in this build (see the file comment).
-  matrix eval(matrix_view) const {
-    throw xeno::error("xylo-hip: model::eval runs on the device only (use a "
-                      "policy_gradient_policy / learner on a bp env)");
+  // nn.h:473-479, on the device (xh_model_eval): the layer chain's forward
+  // over the rows of x with the current parameters (a newer device copy is
+  // pulled first).
+  matrix eval(matrix_view x) const {
+    auto *self = const_cast<model *>(this);
+    self->sync_from_device();
+    std::vector<xh_layer> ls;
+    std::size_t width = x.num_cols(), widest = width;
+    for (const auto &l : layers_) {
+      xh_layer d{0, int(l->input_size()), int(l->output_size())};
+      switch (l->kind()) {
+        case layer_kind::full:
+          d.kind = XH_LAYER_FULL;
+          width = l->output_size();
+          break;
+        case layer_kind::conv1d_1:
+          d.kind = XH_LAYER_CONV1D_1;
+          width = l->input_size() ? width / l->input_size() * l->output_size()
+                                  : width;
+          break;
+        case layer_kind::relu: d.kind = XH_LAYER_RELU; break;
+        case layer_kind::softmax: d.kind = XH_LAYER_SOFTMAX; break;
+        case layer_kind::softmax_xent: d.kind = XH_LAYER_SOFTMAX_XENT; break;
+      }
+      widest = std::max(widest, width);
+      ls.push_back(d);
+    }
+    std::vector<float> p;
+    p.reserve(parameter_size());
+    for (const auto &l : layers_) {
+      vector_view v = l->parameters();
+      p.insert(p.end(), v.begin(), v.end());
+    }
+    std::vector<float> out(x.num_rows() * widest);
+    int oc = 0;
+    if (xh_model_eval(detail::hip_context(), ls.data(), int(ls.size()),
+                      p.data(), p.size(), x.flatten().data(),
+                      int(x.num_rows()), int(x.num_cols()), out.data(),
+                      out.size(), &oc) != XH_OK)
+      throw xeno::error(std::string("xylo-hip: model::eval: ") +
+                        xh_last_error());
+    return matrix(matrix_view(out.data(), x.num_rows(), std::size_t(oc)));
   }
 
   // ---- device binding (used by the device session) ----------------------

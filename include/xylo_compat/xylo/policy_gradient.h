@@ -119,7 +119,10 @@ class kl_ppo_learner : public actor_critic_learner<A, S> {
   learner_kind kind() const override { return learner_kind::kl_ppo; }
 };
 
-// Stochastic policy (policy_gradient.h:338-353): the device samples.
+// Stochastic policy (policy_gradient.h:338-353).  Batched play
+// (agent::play_steps on bp envs) samples inside the device rollout; a single
+// react() on a host state evaluates the model on the device (model::eval ->
+// xh_model_eval) and samples from the global engine as the reference does.
 template <typename A, typename S>
 class policy_gradient_policy : public policy<A, S> {
  public:
@@ -127,16 +130,21 @@ class policy_gradient_policy : public policy<A, S> {
   model &device_model() const { return m_; }
 
  protected:
-  A react(const S &) const override {
-    throw xeno::error("xylo-hip: policy_gradient_policy acts on the device "
-                      "(agent::play_steps), not through react()");
+  A react(const S &state) const override {
+    vector v = to_vector(state);
+    matrix out = m_.eval(fold<2>(vector_view(v), {1, v.size()}));
+    A action;
+    action.from_vector(flatten(out));
+    return action;
   }
 
  private:
   model &m_;
 };
 
-// Argmax policy (policy_gradient.h:356-373): the device evaluates.
+// Argmax policy (policy_gradient.h:356-373): episodes play on the device
+// (agent::play_one_episode on bp envs); react() on a host state evaluates on
+// the device and takes the argmax.
 template <typename A, typename S>
 class policy_gradient_deterministic_policy : public policy<A, S> {
  public:
@@ -144,9 +152,12 @@ class policy_gradient_deterministic_policy : public policy<A, S> {
   model &device_model() const { return m_; }
 
  protected:
-  A react(const S &) const override {
-    throw xeno::error("xylo-hip: policy_gradient_deterministic_policy acts on "
-                      "the device (agent::play_one_episode)");
+  A react(const S &state) const override {
+    vector v = to_vector(state);
+    matrix out = m_.eval(fold<2>(vector_view(v), {1, v.size()}));
+    A action;
+    action.from_vector_deterministic(flatten(out));
+    return action;
   }
 
  private:

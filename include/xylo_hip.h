@@ -313,7 +313,28 @@ int xh_venv_observe(xh_venv *v);
 /* Waits for the venv's work; XH_ERR_INVALID if an action was out of range. */
 int xh_venv_synchronize(xh_venv *v);
 
-/* sizeof of the ABI structs ("xh_config", "xh_eval"; 0 if unknown), so a
+/* ------------------------------------------------------ model::eval -- */
+/* xylo::model::eval (nn.h:473-479) of a layer chain on the device: rows x
+ * cols host floats in, rows x out_cols host floats out.  Layers (nn.h):
+ * full_layer (60-110) and convolution1d_1_layer (113-194, the same Dense
+ * over each of the cols / in points of a row), relu (350-377), softmax
+ * (379-422, no max shift) and softmax_cross_entropy (424-431, forward =
+ * softmax).  params: the flat model::parameters() layout (nn.h:499-508).
+ * Synchronous; for host-side callers of model::eval (the drop-in layer's
+ * policies on host states, evaluation tools). */
+enum { XH_LAYER_FULL = 0, XH_LAYER_CONV1D_1 = 1, XH_LAYER_RELU = 2,
+       XH_LAYER_SOFTMAX = 3, XH_LAYER_SOFTMAX_XENT = 4 };
+typedef struct {
+  int kind;
+  int in, out; /* dense layers: input / output features (per point) */
+} xh_layer;
+int xh_model_eval(xh_ctx *ctx, const xh_layer *layers, int nlayers,
+                  const float *params, size_t nparams, const float *x,
+                  int rows, int cols, float *out, size_t out_cap,
+                  int *out_cols);
+
+/* sizeof of the ABI structs ("xh_config", "xh_eval", "xh_layer"; 0 if
+ * unknown), so a
  * foreign-language binding can check its mirror of them. */
 size_t xh_struct_size(const char *name);
 

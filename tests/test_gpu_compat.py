@@ -132,3 +132,26 @@ def test_example_driver_64_bins():
                             dict(os.environ, XYLO_SEED="3"), timeout=300)
     assert got and got[0][0] == 50 and got[0][1] > 1.0, text[-1000:]
     assert "env-steps/s" in text
+
+
+@pytest.mark.skipif(not os.path.exists(app("bound_env_by_hand")),
+                    reason="build/compat/bound_env_by_hand not built (make compat)")
+def test_bound_env_by_hand_matches_reference():
+    """tests/compat/bound_env_by_hand.cc: after two device-trained windows,
+    environment::apply / reset / view of the device-bound envs, a host
+    random_policy agent stepping one of them, a stochastic policy's react on a
+    host env (model::eval on the device + engine sampling) and model::eval
+    itself print exactly what the real reference prints (golden from the same
+    source built against /root/reference); probabilities within 1e-4."""
+    import subprocess
+    out = subprocess.run([app("bound_env_by_hand")], capture_output=True,
+                         text=True, timeout=300, check=True).stdout.splitlines()
+    want = [str(s) for s in golden("bound_env_by_hand")["lines"]]
+    assert len(out) == len(want), out
+    for got, ref in zip(out, want):
+        if ref.startswith("probs"):
+            a = np.array([float(v) for v in got.split()[1:]])
+            b = np.array([float(v) for v in ref.split()[1:]])
+            assert np.abs(a - b).max() <= 1e-4, (got, ref)
+        else:
+            assert got == ref, (got, ref)
