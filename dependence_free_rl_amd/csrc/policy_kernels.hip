@@ -1126,6 +1126,14 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   // fewer than accB2[16] (spills 344 -> 272 B per lane).  The 64-row kernel
   // keeps the adds in the layer-3 phase (measured 0.1% faster there).
   constexpr bool kB2Late = S::HG > 1;
+  // kMW1 (128-row groups): dW1 and db1 are not per-lane VALU sums but one
+  // v_mfma_f32_16x16x4_f32 GEMM per half-group, dW1^T[f][i] = sum_r X[r][f]
+  // dA1[r][i] with X = [bins/8, item/8, 1], over an LDS image of dA1 (the
+  // freed H1 image) -- 80 accumulator registers fewer (the D=3 variant
+  // spilled 208-340 B per lane), 4 more for the wave's 16-feature tile.
+  constexpr bool kMW1 = S::HG > 1;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 accW1m = {0.0f, 0.0f, 0.0f, 0.0f};
   float b2s = 0.0f;
   float accW1[16][S::D], sA[16], sB[16], accW3[16], accB2[16], accB3 = 0.0f;
 #pragma unroll
@@ -1368,7 +1376,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
       const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
-#pragma unroll
+#pragma unroll (S::HG > 1 ? 4 : 8)  // 128-row groups: 0 B spill (8 at 8)
       for (int s4 = 0; s4 < 8; ++s4) {
         if (XH_ABL(a, 32)) break;
         const float4 av = lds4(pa + 4 * s4);
@@ -1388,10 +1396,41 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
           const int j = 2 * s4 + jj;
           // relu' from the H1 image (post-relu > 0 <=> pre > 0)
           const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
-          sA[j] = fmaf(d, fa, sA[j]);
-          sB[j] = fmaf(d, fb, sB[j]);
+          if constexpr (kMW1) {
+            dh[j] = d;  // dA1, imaged below
+          } else {
+            sA[j] = fmaf(d, fa, sA[j]);
+            sB[j] = fmaf(d, fb, sB[j]);
 #pragma unroll
-          for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
+            for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
+          }
+        }
+      }
+      if constexpr (kMW1) {
+        // ---- dW1 / db1 of this half-group by MFMA (see kMW1 above)
+        __syncthreads();  // every wave is done with the H1 / dA2 images
+        float *A1T = H1T;  // [H1][TS]: dA1 transposed (feature-major)
+        float *XT = DAT;   // [F0 + 1][TS]: X transposed, row 2D = ones
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          A1T[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = dh[j];
+        if (q == 0) {
+#pragma unroll
+          for (int f = 0; f < S::F0; ++f) XT[f * S::TS + rt * 32 + lr] = feat(f);
+          XT[S::F0 * S::TS + rt * 32 + lr] = 1.0f;
+        }
+        __syncthreads();
+        // wave w: feature tile i = 16w .. 16w+15; M = f (16, F0 + 1 used),
+        // N = i, K = the 64 rows in 16 steps of 4 (lane quarter kq = row
+        // 4s + kq): A[f][k] = X[row][f], B[k][i] = dA1[row][i]
+        const int fi = lane & 15, kq = lane >> 4;
+        const float *xa = XT + fi * S::TS + kq;
+        const float *ab = A1T + (w * 16 + fi) * S::TS + kq;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const float av = fi <= S::F0 ? xa[4 * s] : 0.0f;
+          accW1m = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ab[4 * s], accW1m,
+                                                       0, 0, 0);
         }
       }
     }
@@ -1438,14 +1477,16 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
     if (lr == 0) {
       const int i = q * 32 + acc_row(j, h);
+      if constexpr (!kMW1) {
 #pragma unroll
-      for (int f = 0; f < S::D; ++f) my[i * S::F0 + f] = vw1[f];
+        for (int f = 0; f < S::D; ++f) my[i * S::F0 + f] = vw1[f];
 #pragma unroll
-      for (int d = 0; d < S::D; ++d)
-        my[i * S::F0 + S::D + d] =
-            va * ((float)a.env.item_a[d] / (float)kCapacity) +
-            vb * ((float)a.env.item_b[d] / (float)kCapacity);
-      my[S::H1 * S::F0 + i] = va + vb;
+        for (int d = 0; d < S::D; ++d)
+          my[i * S::F0 + S::D + d] =
+              va * ((float)a.env.item_a[d] / (float)kCapacity) +
+              vb * ((float)a.env.item_b[d] / (float)kCapacity);
+        my[S::H1 * S::F0 + i] = va + vb;
+      }
       my[S::H1 * S::F0 + S::H1 + i] = vw3;  // o2 = q*32 + acc_row too
       if (!kB2Late) my[S::H1 * S::F0 + S::H1 + S::H2 + i] = vb2;
     }
@@ -1461,7 +1502,19 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     if (lane == 0) my[S::RED - 1] = w == 0 ? v : 0.0f;
   }
   __syncthreads();
+  if constexpr (kMW1) {  // dW1^T tile of wave w: rows f = 4 kq + r, col i
+    const int fi = lane & 15, kq = lane >> 4, i = w * 16 + fi;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * kq + r;
+      if (f < S::F0)
+        slab[L.oW1() + i * S::F0 + f] = accW1m[r];
+      else if (f == S::F0)
+        slab[L.ob1() + i] = accW1m[r];
+    }
+  }
   for (int i = threadIdx.x; i < S::RED; i += blockDim.x) {
+    if (kMW1 && i < S::H1 * S::F0 + S::H1) continue;  // written above
     float v = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += scr[k * S::RED + i];

@@ -49,7 +49,7 @@ int main() {
   bp::ppo_learner learner(rb, actor, aopt, value, vopt);
   xylo::policy_gradient_policy<bp::action, bp::observation> pol(actor);
 
-  const int W = 4;
+  const int W = 8;  // the device trainer packs 64 / num_bins envs per group
   std::vector<std::unique_ptr<bp::environment>> envs;
   std::vector<std::unique_ptr<bp::agent>> agents;
   for (int i = 0; i < W; ++i) envs.push_back(std::make_unique<bp::environment>());

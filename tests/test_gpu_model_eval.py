@@ -37,7 +37,7 @@ def test_full_mlps_match_oracle(ctx, kind):
                   ("relu", 0, 0), ("full", 32, 1)]
         om = po.full_model(256, [64, 32], 1)
     else:
-        p = init_full_policy(B, D, (256, 128), seed=6) * 50.0
+        p = init_full_policy(B, D, (256, 128), seed=6) * 3.0
         layers = [("full", 256, 256), ("relu", 0, 0), ("full", 256, 128),
                   ("relu", 0, 0), ("full", 128, B), ("softmax_xent", 0, 0)]
         om = po.full_model(256, [256, 128], B, po.OR_SOFTMAX_XENT)
