@@ -1,6 +1,6 @@
 // Test program, built twice: against the real reference headers (the golden
 // run, tests/golden/make_compat_golden.py) and against include/xylo_compat
-// (the device run, tests/test_gpu_compat.py).  It trains 4 agents for two
+// (the device run, tests/test_gpu_compat.py).  It trains 8 agents for two
 // windows (their envs then live on the device in the drop-in build), then
 // drives those envs BY HAND through the reference API -- environment::apply /
 // reset / view (bin_packing.h:53-70), a host random_policy agent stepping one
