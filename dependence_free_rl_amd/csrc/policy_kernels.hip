@@ -462,6 +462,104 @@ __global__ __launch_bounds__(512, 4) void rollout_wave_kernel(RolloutArgs a) {
   }
 }
 
+// Softmax of one env's 128 candidate-bin scores (lane holds bins lane and
+// 64 + lane: z[0], z[1]), the categorical sample (sequential
+// discrete_distribution order, the exact restatement near a boundary) or the
+// forced action, and the env transition into slot t+1 -- one wave.
+template <class S>
+__device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
+                                               const float (&z)[2]) {
+  const int lane = threadIdx.x & 63;
+  const int N = a.b.N, t = a.t;
+  float p[2];
+  float se = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    p[k] = expf(z[k]);
+    se += p[k];
+  }
+  se = seg_sum<64>(se);
+  p[0] = p[0] / se;
+  p[1] = p[1] / se;
+  if (a.logits_out) {
+    a.logits_out[(size_t)env * 128 + lane] = z[0];
+    a.logits_out[(size_t)env * 128 + 64 + lane] = z[1];
+  }
+  if (a.probs_out) {
+    a.probs_out[(size_t)env * 128 + lane] = p[0];
+    a.probs_out[(size_t)env * 128 + 64 + lane] = p[1];
+  }
+  uint32_t x = a.b.rng[env];
+  int choice;
+  if (a.forced) {
+    choice = a.forced[(size_t)t * N + env];
+    (void)canonical(x);
+  } else {
+    const double pd0 = (double)p[0], pd1 = (double)p[1];
+    const double sd = seg_sum_d<64>(pd0 + pd1);
+    const double c0 = seg_scan_d<64>(pd0 / sd, lane);
+    const double tot0 = wave_shfl_d(c0, 63);
+    double c1 = tot0 + seg_scan_d<64>(pd1 / sd, lane);
+    if (lane == 63) c1 = 1.0;
+    const double u = canonical(x);
+    choice = __popcll(__ballot(c0 < u)) + __popcll(__ballot(c1 < u));
+    const float gap = (float)fmin(fabs(c0 - u), fabs(c1 - u));
+    if (seg_min<64>(gap) < 1e-9f) {  // exact sequential restatement
+      double s2 = 0.0;
+      for (int k = 0; k < 128; ++k)
+        s2 += (double)wave_shfl(p[k >> 6], k & 63);
+      double acc = 0.0;
+      int c2 = 127;
+      for (int k = 0; k < 128; ++k) {
+        const double qk = (double)wave_shfl(p[k >> 6], k & 63) / s2;
+        acc = k == 0 ? qk : acc + qk;
+        const double cpk = k == 127 ? 1.0 : acc;
+        if (!(cpk < u) && k < c2) c2 = k;
+      }
+      choice = c2;
+    }
+  }
+  const float pold = choice < 64 ? wave_shfl(p[0], choice)
+                                 : wave_shfl(p[1], choice - 64);
+  const size_t e = (size_t)t * N + env;
+  const int8_t *ip = a.b.items + e * 4;
+  int iv[S::D];
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) iv[d] = ip[d];
+  int nb[2][S::D];
+  int neg[2] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int bin = k * 64 + lane;
+    const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      nb[k][d] = bin == choice ? bp[d] - iv[d] : bp[d];
+      neg[k] |= nb[k][d] < 0;
+    }
+  }
+  const int done = __shfl(choice < 64 ? neg[0] : neg[1], choice & 63, kWave);
+  const bool first = canonical(x) < a.env.p_a;
+  const size_t o = (size_t)(t + 1) * N + env;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    int8_t *ob = a.b.bins + o * S::BD + (k * 64 + lane) * S::D;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d)
+      ob[d] = (int8_t)(done ? kCapacity : nb[k][d]);
+  }
+  if (lane == 0) {
+    int8_t *oi = a.b.items + o * 4;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
+    a.b.action[(size_t)t * N + env] = choice;
+    a.b.pold[(size_t)t * N + env] = pold;
+    a.b.done[(size_t)t * N + env] = (uint8_t)done;
+    a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
+  }
+}
+
 // ================================================ rollout step, 128 bins ===
 // One env per group (B = 128 = two 64-row half-groups, BASELINE config 5).
 // Forward as rollout_step_kernel per half-group, scores of all 128
@@ -509,99 +607,122 @@ __global__ __launch_bounds__(256, 2) void rollout_step128_kernel(RolloutArgs a) 
     }
     __syncthreads();
     if (w == 0) {
-      float z[2], p[2];
-      float se = 0.0f;
+      float z[2];
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         float zs = 0.0f;
 #pragma unroll
         for (int o = 0; o < S::NOT; ++o) zs += lds[S::L_Z + o * R + k * 64 + lane];
         z[k] = zs + lds[S::L_B3];
-        p[k] = expf(z[k]);
-        se += p[k];
       }
-      se = seg_sum<64>(se);
-      p[0] = p[0] / se;
-      p[1] = p[1] / se;
-      if (a.logits_out) {
-        a.logits_out[(size_t)env * 128 + lane] = z[0];
-        a.logits_out[(size_t)env * 128 + 64 + lane] = z[1];
-      }
-      if (a.probs_out) {
-        a.probs_out[(size_t)env * 128 + lane] = p[0];
-        a.probs_out[(size_t)env * 128 + 64 + lane] = p[1];
-      }
-      uint32_t x = a.b.rng[env];
-      int choice;
-      if (a.forced) {
-        choice = a.forced[(size_t)t * N + env];
-        (void)canonical(x);
-      } else {
-        const double pd0 = (double)p[0], pd1 = (double)p[1];
-        const double sd = seg_sum_d<64>(pd0 + pd1);
-        const double c0 = seg_scan_d<64>(pd0 / sd, lane);
-        const double tot0 = wave_shfl_d(c0, 63);
-        double c1 = tot0 + seg_scan_d<64>(pd1 / sd, lane);
-        if (lane == 63) c1 = 1.0;
-        const double u = canonical(x);
-        choice = __popcll(__ballot(c0 < u)) + __popcll(__ballot(c1 < u));
-        const float gap = (float)fmin(fabs(c0 - u), fabs(c1 - u));
-        if (seg_min<64>(gap) < 1e-9f) {  // exact sequential restatement
-          double s2 = 0.0;
-          for (int k = 0; k < 128; ++k)
-            s2 += (double)wave_shfl(p[k >> 6], k & 63);
-          double acc = 0.0;
-          int c2 = 127;
-          for (int k = 0; k < 128; ++k) {
-            const double qk = (double)wave_shfl(p[k >> 6], k & 63) / s2;
-            acc = k == 0 ? qk : acc + qk;
-            const double cpk = k == 127 ? 1.0 : acc;
-            if (!(cpk < u) && k < c2) c2 = k;
-          }
-          choice = c2;
-        }
-      }
-      const float pold = choice < 64 ? wave_shfl(p[0], choice)
-                                     : wave_shfl(p[1], choice - 64);
-      const size_t e = (size_t)t * N + env;
-      const int8_t *ip = a.b.items + e * 4;
-      int iv[S::D];
-#pragma unroll
-      for (int d = 0; d < S::D; ++d) iv[d] = ip[d];
-      int nb[2][S::D];
-      int neg[2] = {0, 0};
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int bin = k * 64 + lane;
-        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
-#pragma unroll
-        for (int d = 0; d < S::D; ++d) {
-          nb[k][d] = bin == choice ? bp[d] - iv[d] : bp[d];
-          neg[k] |= nb[k][d] < 0;
-        }
-      }
-      const int done = __shfl(choice < 64 ? neg[0] : neg[1], choice & 63, kWave);
-      const bool first = canonical(x) < a.env.p_a;
-      const size_t o = (size_t)(t + 1) * N + env;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        int8_t *ob = a.b.bins + o * S::BD + (k * 64 + lane) * S::D;
-#pragma unroll
-        for (int d = 0; d < S::D; ++d)
-          ob[d] = (int8_t)(done ? kCapacity : nb[k][d]);
-      }
-      if (lane == 0) {
-        int8_t *oi = a.b.items + o * 4;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-          oi[d] = d < S::D ? (int8_t)(first ? a.env.item_a[d] : a.env.item_b[d]) : 0;
-        a.b.action[(size_t)t * N + env] = choice;
-        a.b.pold[(size_t)t * N + env] = pold;
-        a.b.done[(size_t)t * N + env] = (uint8_t)done;
-        a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
-      }
+      sample_step128<S>(a, env, z);
     }
     __syncthreads();
+  }
+}
+
+// ========================================= rollout step, 128 bins, wave/env ==
+// B = 128, [128,128] (config 5): one wave per env, the wave_kernel scheme
+// over the env's two 64-row half-groups in turn (every layer operation and
+// its order as rollout_step128_kernel's, so logits and actions are
+// bit-identical), then the wave samples its own env: no barrier between the
+// forward and the sampler and four waves per SIMD to hide the
+// double-precision sampler under the other waves' MFMAs.
+template <class S>
+__global__ __launch_bounds__(512, 4) void rollout_wave128_kernel(RolloutArgs a) {
+  static_assert(S::B == 128 && S::NIT == 4 && S::NOT == 4,
+                "wave rollout: B=128, [128,128]");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  stage_params<S>(a.params, lds);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int wpb = blockDim.x >> 6;
+  const int N = a.b.N, t = a.t;
+  for (int env = blockIdx.x * wpb + w; env < N; env += gridDim.x * wpb) {
+    float z0 = 0.0f, z1 = 0.0f;
+#pragma unroll 1
+    for (int hg = 0; hg < 2; ++hg) {
+      RowRaw<S> cur;
+      const size_t e = (size_t)t * N + env;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int bin = hg * 64 + rt * 32 + lr;
+        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
+        const int8_t *ip = a.b.items + e * 4;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          cur.bv[rt][d] = bp[d];
+          cur.iv[rt][d] = ip[d];
+        }
+      }
+      float xb[2][S::S1];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
+      float zl[2] = {0.0f, 0.0f};
+#pragma unroll 1
+      for (int o2t = 0; o2t < 4; ++o2t) {
+        const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
+        f32x16 pre[2];
+        pre[0] = zero16();
+        pre[1] = zero16();
+#pragma unroll 1
+        for (int it = 0; it < 4; ++it) {
+          f32x16 t1[2];
+          t1[0] = zero16();
+          t1[1] = zero16();
+#pragma unroll
+          for (int s = 0; s < S::S1; ++s) {
+            const int k = 2 * s + h;
+            const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+            t1[0] = mfma32(wa, xb[0][s], t1[0]);
+            t1[1] = mfma32(wa, xb[1][s], t1[1]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * q + 4 * h);
+            const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              t1[0][4 * q + u] = relu(t1[0][4 * q + u] + bq[u]);
+              t1[1][4 * q + u] = relu(t1[1][4 * q + u] + bq[u]);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 a4 = lds4(wrow + it * 32 + 8 * q);
+            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              pre[0] = mfma32(av[u], t1[0][4 * q + u], pre[0]);
+              pre[1] = mfma32(av[u], t1[1][4 * q + u], pre[1]);
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bb = lds4(lds + S::L_B2 + o2t * 32 + 8 * q + 4 * h);
+          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            pre[0][4 * q + u] += bq[u];
+            pre[1][4 * q + u] += bq[u];
+          }
+        }
+        zl[0] += logit_part<S>(lds, pre[0], o2t);
+        zl[1] += logit_part<S>(lds, pre[1], o2t);
+      }
+      // lane = row of the half-group = bin hg*64 + lane
+      const float zh = (h ? zl[1] : zl[0]) + lds[S::L_B3];
+      if (hg == 0)
+        z0 = zh;
+      else
+        z1 = zh;
+    }
+    const float z[2] = {z0, z1};
+    sample_step128<S>(a, env, z);
   }
 }
 
@@ -1619,6 +1740,22 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
       attr = true;                                                           \
     }                                                                        \
     const int ng = a.b.N / S::G;                                             \
+    if constexpr (S::B == 128 && S::NIT == 4 && S::NOT == 4) {               \
+      if (!rollout4()) {                                                     \
+        static bool wattr = false;                                           \
+        if (!wattr) {                                                        \
+          (void)hipFuncSetAttribute((const void *)rollout_wave128_kernel<S>, \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                    (int)rollout_lds<S>());                  \
+          wattr = true;                                                      \
+        }                                                                    \
+        const int wg = (a.b.N + 7) / 8;                                      \
+        hipLaunchKernelGGL(rollout_wave128_kernel<S>,                        \
+                           dim3(grid < wg ? grid : wg), dim3(512),           \
+                           rollout_lds<S>(), s, a);                          \
+        return hipGetLastError();                                            \
+      }                                                                      \
+    }                                                                        \
     if constexpr (S::B == 64 && S::NIT == 4 && S::NOT == 4) {                \
       if (!rollout4()) {                                                     \
         static bool wattr = false;                                           \

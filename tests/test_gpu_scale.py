@@ -152,17 +152,18 @@ def test_c3_rng_positions_full_size(ctx):
     np.testing.assert_array_equal(rng, want)
 
 
-def test_wave_rollout_matches_4wave(ctx, monkeypatch):
-    """Full config-3 size: the wave-per-env rollout (default at B=64,
-    [128,128]) and the 4-wave rollout (XH_ROLLOUT_KERNEL=4) produce
-    the same trajectories (actions, states, items, dones) and RNG states on
-    the same parameters (T = 4 steps of 32768 envs); logits / probabilities
-    agree to the last place."""
+@pytest.mark.parametrize("algo,N,B,D,T", [("ppo", 32768, 64, 2, 4),
+                                         ("ac", 16384, 128, 3, 8)])
+def test_wave_rollout_matches_4wave(ctx, monkeypatch, algo, N, B, D, T):
+    """Full config-3 / config-5 size: the wave-per-env rollouts (default at
+    B=64 and B=128, [128,128]) and the 4-wave rollouts (XH_ROLLOUT_KERNEL=4)
+    produce the same trajectories (actions, states, items, dones) and RNG
+    states on the same parameters; logits / probabilities agree to the last
+    place."""
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
                                                 BUF_ITEMS, BUF_LOGITS, BUF_POLD,
                                                 BUF_PROBS, BUF_RNG)
-    N, B, D, T = 32768, 64, 2, 4
     pp, vp = init_policy(D, 128, 128, seed=11), init_value(B, D, seed=12)
     bufs = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_LOGITS, BUF_POLD,
             BUF_PROBS, BUF_RNG)
@@ -170,12 +171,13 @@ def test_wave_rollout_matches_4wave(ctx, monkeypatch):
     for kern in ("wave", "4"):
         if kern == "4":
             monkeypatch.setenv("XH_ROLLOUT_KERNEL", "4")
-        tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T,
+        tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
                      widths=(128, 128), rng_state=99)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         tr.rollout()
         got[kern] = [tr.buffer(b).copy() for b in bufs]
+        tr.close()
     exact = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_RNG)
     for b, x, y in zip(bufs, got["wave"], got["4"]):
         if b in exact:
