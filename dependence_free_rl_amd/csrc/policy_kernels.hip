@@ -1342,6 +1342,33 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
     return pre;
   };
+  // Layer-1 tile q of this wave's rows into the H1 image only: the same
+  // operations as forward()'s it == q step, so the image is bit-identical
+  // (128-row groups: the earlier half-group's H1 image is rebuilt from here
+  // while its layer-2 pre-activations stay in registers).
+  auto write_h1_tile = [&]() {
+    float xb[S::S1];
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
+    f32x16 t1;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const float4 bb = lds4(lds + S::L_B1 + q * 32 + 8 * qq + 4 * h);
+      t1[4 * qq + 0] = bb.x;
+      t1[4 * qq + 1] = bb.y;
+      t1[4 * qq + 2] = bb.z;
+      t1[4 * qq + 3] = bb.w;
+    }
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) {
+      const int k = 2 * s + h;
+      const float wa = k < S::F0 ? lds[S::L_W1 + (q * 32 + lr) * S::F0 + k] : 0.0f;
+      t1 = mfma32(wa, xb[s], t1);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      H1T[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = relu(t1[j]);
+  };
 
   if (HG == 1 && (int)blockIdx.x < ngroups) fetch_row(blockIdx.x, 0, bv_c, iv_c);
 
@@ -1359,13 +1386,14 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
 
     // ---- forward (all R rows) -> per-tile partial logits in LDS
-    f32x16 pre;
+    f32x16 pre, pre0;
 #pragma unroll
     for (int hg = 0; hg < HG; ++hg) {
       if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
-      // the last half-group's H1 image is written here and its pre-
-      // activations stay in registers for the backward
+      // the last half-group's H1 image is written here; every half-group's
+      // pre-activations stay in registers for the backward
       pre = forward(hg == HG - 1);
+      if (HG > 1 && hg == 0) pre0 = pre;
       const float zp = logit_part<S, true>(lds, pre, q);
       if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
     }
@@ -1438,15 +1466,17 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
 
     // backward, last half-group first: it reuses the forward's registers and
-    // H1 image; the earlier half-groups recompute their forward (a second
-    // 64-row H1 image does not fit in LDS beside W2 and the dA2 image)
+    // H1 image; the earlier half-group keeps its layer-2 pre-activations in
+    // registers and rebuilds only its H1 image (layer 1: a second 64-row
+    // image does not fit in LDS beside W2 and the dA2 image)
 #pragma unroll
     for (int hb = 0; hb < HG; ++hb) {
       const int hg = HG - 1 - hb;
       if (hb > 0) {
         __syncthreads();  // previous half-group's images consumed
         fetch_row(g, hg, bv_c, iv_c);
-        pre = forward(true);
+        write_h1_tile();  // the H1 image again (layer 1 only)
+        pre = pre0;       // layer 2 kept from the forward
       }
       // ---- backward through layer 3 and the layer-2 relu
       {

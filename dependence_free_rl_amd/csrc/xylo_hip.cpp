@@ -230,7 +230,10 @@ template <class P>
 int dalloc(xh_trainer *t, P **p, size_t bytes) {
   void *q = nullptr;
   HIPCHK(hipMalloc(&q, bytes < 16 ? 16 : bytes));
-  HIPCHK(hipMemset(q, 0, bytes < 16 ? 16 : bytes));
+  // zeroed on the trainer's stream: a null-stream hipMemset is not ordered
+  // before the non-blocking stream's next copy / kernel (measured: the zero
+  // fill landing after the parameter upload, intermittently)
+  HIPCHK(hipMemsetAsync(q, 0, bytes < 16 ? 16 : bytes, t->ctx->stream));
   t->allocs.push_back(q);
   *p = reinterpret_cast<P *>(q);
   return XH_OK;
@@ -326,19 +329,20 @@ void *buffer_ptr(const xh_trainer *t, int which) {
   return nullptr;
 }
 
-// Copies between the device and caller (pageable) host memory: drain the
-// stream, then a blocking hipMemcpy.  An asynchronous copy into or out of
-// pageable memory is staged by the runtime, and reading the host array right
-// after the stream synchronisation was measured to return stale entries on
-// ROCm 7.2 (evaluate traces differing between identical calls).
+// Copies between the device and caller (pageable) host memory, ordered on
+// the trainer's stream and waited for before returning (the caller may free
+// or read its buffer right after).  Not hipMemcpy: the trainer's stream is
+// non-blocking, so a null-stream H2D copy of pageable memory, which returns
+// once the bytes are staged, is not ordered before the next kernel on it --
+// measured: parameters read stale by the first rollout kernel, intermittently.
 hipError_t copy_to_host(void *host, const void *dev, size_t n, hipStream_t s) {
-  const hipError_t e = hipStreamSynchronize(s);
-  return e != hipSuccess ? e : hipMemcpy(host, dev, n, hipMemcpyDeviceToHost);
+  const hipError_t e = hipMemcpyAsync(host, dev, n, hipMemcpyDeviceToHost, s);
+  return e != hipSuccess ? e : hipStreamSynchronize(s);
 }
 hipError_t copy_to_device(void *dev, const void *host, size_t n,
                           hipStream_t s) {
-  const hipError_t e = hipStreamSynchronize(s);
-  return e != hipSuccess ? e : hipMemcpy(dev, host, n, hipMemcpyHostToDevice);
+  const hipError_t e = hipMemcpyAsync(dev, host, n, hipMemcpyHostToDevice, s);
+  return e != hipSuccess ? e : hipStreamSynchronize(s);
 }
 
 int copy_ok(hipError_t e) {
@@ -1187,7 +1191,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
       return st;
     }
     if (st == XH_OK && t->beta)
-      st = copy_ok(hipMemcpy(t->beta, &c.kl_beta, 4, hipMemcpyHostToDevice));
+      st = copy_ok(copy_to_device(t->beta, &c.kl_beta, 4, ctx->stream));
     t->opt[XH_POLICY].lr = c.lr_policy;
     t->opt[XH_POLICY].wd = c.wd_policy;
     t->opt[XH_VALUE].lr = c.lr_value;
@@ -1681,11 +1685,11 @@ int xh_venv_create(xh_ctx *ctx, int num_envs, int bins, int dims,
     for (int b = 0; b < XH_VENV_BUF_COUNT && st == XH_OK; ++b) {
       v->bytes[b] = sz[b];
       if (hipMalloc(&v->buf[b], sz[b]) != hipSuccess ||
-          hipMemset(v->buf[b], 0, sz[b]) != hipSuccess)
+          hipMemsetAsync(v->buf[b], 0, sz[b], ctx->stream) != hipSuccess)
         st = fail(XH_ERR_HIP, "venv: allocating %zu bytes", sz[b]);
     }
     if (st == XH_OK && (hipMalloc((void **)&v->err, 4) != hipSuccess ||
-                        hipMemset(v->err, 0, 4) != hipSuccess))
+                        hipMemsetAsync(v->err, 0, 4, ctx->stream) != hipSuccess))
       st = fail(XH_ERR_HIP, "venv: error flag");
     if (st == XH_OK) {
       uint32_t x0 = rng_state % 2147483647u;
@@ -1738,7 +1742,8 @@ int venv_check_err(xh_venv *v) {
   HIPCHK(copy_to_host(&err, v->err, 4, v->ctx->stream));
   HIPCHK(hipStreamSynchronize(v->ctx->stream));
   if (err) {
-    HIPCHK(hipMemset(v->err, 0, 4));
+    HIPCHK(hipMemsetAsync(v->err, 0, 4, v->ctx->stream));
+    HIPCHK(hipStreamSynchronize(v->ctx->stream));
     return fail(XH_ERR_INVALID, "venv: an action was outside [0, %d); those "
                 "envs were left untouched", v->env.B);
   }
