@@ -24,7 +24,9 @@
 // supplies `gen_env<B,D>`: the same environment semantics generalised to B bins
 // and D dims (capacity 8 per dim; items (4,2)/(1,2) at D=2, (4)/(1) at D=1,
 // (4,2,2)/(1,2,1) at D=3; P(first)=0.4).  mode=envcheck proves gen_env<8,2>
-// produces bit-identical trajectories and RNG consumption to bp::environment.
+// produces bit-identical trajectories and RNG consumption to bp::environment,
+// and that gen_env<64,2> / gen_env<128,2> reproduce it on any 8 of their bins
+// (envcheck_injected).  D = 1 and D = 3 have no reference env to compare with.
 #include <apps/bin_packing/bin_packing.h>  // pulls xylo/nn.h, rl.h, policy_gradient.h
 
 #include <xeno/sys/file_descriptor.h>
@@ -49,6 +51,7 @@ namespace ref_minwaste {
 #undef main
 }  // namespace ref_minwaste
 
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -406,7 +409,69 @@ int mode_rng(std::map<std::string, std::string> &a) {
 }
 
 // ------------------------------------------------------- mode: envcheck ----
-// bp::environment (the reference env) vs gen_env<8,2>: identical trajectories.
+// A uniform 8-way choice (random_policy<8>'s react: the same engine draws)
+// placed on 8 distinct bins `slot` of a B-bin env.
+template <std::size_t B>
+class injected_policy
+    : public xylo::policy<xylo::discrete_action<B>, gen_obs<B, 2>> {
+public:
+  explicit injected_policy(const std::vector<int> &slot) : slot_(slot) {}
+  xylo::discrete_action<B> react(const gen_obs<B, 2> &) const override {
+    xylo::random_policy<8, gen_obs<8, 2>> rp;
+    xylo::discrete_action<B> a;
+    a.choice = slot_[rp.react(gen_obs<8, 2>{}).choice];
+    return a;
+  }
+
+private:
+  std::vector<int> slot_;
+};
+
+// gen_env<B,2> (B = 64, 128: the benchmark shapes) driven by the reference
+// run's choices placed on 8 random distinct bins: those bins must follow the
+// reference env's 8 bins transition for transition, every other bin must stay
+// full, and rewards, episode ends and the engine must agree.  With the slots
+// redrawn per seed, every bin index of the larger env gets exercised.
+template <std::size_t B>
+bool envcheck_injected(uint32_t seed, long steps, uint32_t x_end,
+                       const std::vector<int32_t> &choice,
+                       const std::vector<int32_t> &reward,
+                       const std::vector<int32_t> &end_bins) {
+  std::vector<int> perm(B);
+  for (std::size_t i = 0; i < B; ++i) perm[i] = (int)i;
+  std::mt19937 pick(seed * 7919u + (uint32_t)B);
+  std::shuffle(perm.begin(), perm.end(), pick);
+  std::vector<int> slot(perm.begin(), perm.begin() + 8);
+
+  auto &g = xylo::default_generator();
+  g.seed(seed);
+  injected_policy<B> pol(slot);
+  gen_env<B, 2> genv(0, nullptr);
+  xylo::replay_buffer<xylo::discrete_action<B>, gen_obs<B, 2>> rb;
+  gen_agent<B, 2> ag(pol, genv, rb);
+  for (long i = 0; i < steps; ++i) ag.step();
+  bool same = engine_state() == x_end;
+  std::vector<int> owner(B, -1);
+  for (int b = 0; b < 8; ++b) owner[slot[b]] = b;
+  std::size_t k = 0;
+  for (auto &traj : rb.sample_td())
+    for (auto &tr : traj) {
+      if (k >= choice.size()) return false;
+      same &= tr.action.choice == (std::size_t)slot[choice[k]];
+      same &= (int)tr.reward == reward[k];
+      for (std::size_t b = 0; b < B; ++b)
+        for (int d = 0; d < 2; ++d) {
+          int want = owner[b] < 0 ? kCapacity
+                                  : end_bins[(k * 8 + owner[b]) * 2 + d];
+          same &= tr.end_state.bins[b][d] == want;
+        }
+      ++k;
+    }
+  return same && k == choice.size();
+}
+
+// bp::environment (the reference env) vs gen_env<8,2>: identical trajectories;
+// vs gen_env<64,2> and gen_env<128,2> through envcheck_injected.
 int mode_envcheck(std::map<std::string, std::string> &a) {
   recorder rec(a["out"]);
   uint32_t seed = iarg(a, "seed", 7);
@@ -474,9 +539,15 @@ int mode_envcheck(std::map<std::string, std::string> &a) {
     }
   same &= k == nt;
   rec.i32("gen_env_identical", {same ? 1 : 0});
-  std::fprintf(stderr, "envcheck: %llu transitions, gen_env identical=%d\n",
-               (unsigned long long)nt, same);
-  return same ? 0 : 1;
+  bool same64 = envcheck_injected<64>(seed, steps, x_end, choice, reward, end_bins);
+  bool same128 = envcheck_injected<128>(seed, steps, x_end, choice, reward, end_bins);
+  rec.i32("gen_env64_identical", {same64 ? 1 : 0});
+  rec.i32("gen_env128_identical", {same128 ? 1 : 0});
+  std::fprintf(stderr,
+               "envcheck: %llu transitions, gen_env identical=%d, "
+               "gen_env<64,2> injected=%d, gen_env<128,2> injected=%d\n",
+               (unsigned long long)nt, same, same64, same128);
+  return same && same64 && same128 ? 0 : 1;
 }
 
 // -------------------------------------------------------- mode: deep -------

@@ -56,7 +56,8 @@ FIXTURES = {
     # (xylo/tensor.cc:71-75, 467-470; apps/bin_packing/bin_packing.h:81)
     "rng": ("rng", ["seed=42", "n=8000"]),
     # bp::environment + bp::agent + random_policy (bin_packing.h:46-107,
-    # rl.h:305-349), and gen_env<8,2> equivalence
+    # rl.h:305-349), and gen_env<8,2> equivalence; gen_env<64,2> and
+    # gen_env<128,2> reproduce it on 8 injected bins
     "env8": ("envcheck", ["seed=7", "steps=3000"]),
     # deep_agent.cc with weights.20, seed 1, 1000 argmax episodes
     "deep_w20": ("deep", ["seed=1", "episodes=1000",

@@ -18,23 +18,37 @@ def _venv(ctx, **kw):
     return VecEnv(ctx, **kw)
 
 
-def test_venv_replays_reference_env8(ctx):
+@pytest.mark.parametrize("B", [8, 64, 128])
+def test_venv_replays_reference_env8(ctx, B):
     """One env, the reference's 3000 random-policy choices: every state,
-    item, reward and the final engine state equal the real reference's."""
+    item, reward and the final engine state equal the real reference's.  At
+    64 / 128 bins the choices land on 8 random distinct bins (the benchmark
+    shapes; the reference env has 8): those bins follow the reference's, the
+    others stay full (the same check the harness makes of gen_env<64|128,2>,
+    oracle/ref_harness.cc envcheck_injected)."""
     from dependence_free_rl_amd._lib import VENV_RNG
     g = golden("env8")
-    env = _venv(ctx, num_envs=1, bins=8, dims=2, rng_state=int(g["x0"][0]),
+    slot = (np.arange(8) if B == 8 else
+            np.random.default_rng(B).permutation(B)[:8])
+    env = _venv(ctx, num_envs=1, bins=B, dims=2, rng_state=int(g["x0"][0]),
                 policy_draws=2)
+
+    def placed(b8):
+        full = np.full((B, 2), 8, dtype=b8.dtype)
+        full[slot] = b8
+        return full
+
     n = len(g["choice"])
     for k in range(n):
         bins, item = env.view()
-        np.testing.assert_array_equal(bins[0], g["start_bins"][k])
+        np.testing.assert_array_equal(bins[0], placed(g["start_bins"][k]))
         np.testing.assert_array_equal(item[0], g["start_item"][k])
-        env.set_actions([g["choice"][k]])
+        env.set_actions([slot[g["choice"][k]]])
         reward, done = env.step()
         assert reward[0] == g["reward"][k] and done[0] == (g["reward"][k] == 0)
         if not done[0]:
-            np.testing.assert_array_equal(env.view()[0][0], g["end_bins"][k])
+            np.testing.assert_array_equal(env.view()[0][0],
+                                          placed(g["end_bins"][k]))
     assert env.get(VENV_RNG)[0] == int(g["x_end"][0])
     env.close()
 

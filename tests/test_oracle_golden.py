@@ -87,6 +87,10 @@ def test_env_trajectory_bit_exact():
             env.reset()
     assert rng.state == int(g["x_end"][0])
     assert int(g["gen_env_identical"][0]) == 1
+    # the benchmark-shape envs (64 / 128 bins) reproduce the reference env on
+    # 8 injected bins, the rest staying full (ref_harness.cc envcheck_injected)
+    assert int(g["gen_env64_identical"][0]) == 1
+    assert int(g["gen_env128_identical"][0]) == 1
 
 
 # ---------------------------------------------------------- deep agent ----
