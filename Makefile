@@ -29,7 +29,7 @@ REF_APPS := ppo_training ac_training ppo2_training pg_training deep_agent \
 EXAMPLES := $(patsubst examples/%.cc,$(COMPAT)/%,$(wildcard examples/*.cc))
 COMPAT_HDRS := $(shell find include/xylo_compat -name '*.h') include/xylo_hip.h
 
-.PHONY: all lib oracle compat clean diag
+.PHONY: all lib oracle compat clean diag variant
 all: lib oracle compat
 
 lib: $(LIB)
@@ -79,3 +79,12 @@ $(COMPAT)/%: examples/%.cc $(COMPAT_HDRS) $(LIB)
 
 clean:
 	rm -f $(OBJS) $(LIB)
+
+# performance variants of the policy kernels for A/B runs on one box
+# (tools/gpu_variants.sh; loaded through XH_LIB_PATH, never by the product):
+#   make variant V=name VFLAGS="-DXH_DIAG_TRACE=1 ..."
+variant: $(OBJS)
+	@mkdir -p build/$(V)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/policy_kernels.hip -o build/$(V)/policy_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/$(V)/libxylo_hip.so build/$(V)/policy_kernels.o \
+	    $(filter-out $(SRC)/policy_kernels.o,$(OBJS)) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

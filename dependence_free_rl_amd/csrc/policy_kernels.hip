@@ -33,10 +33,31 @@
 // XH_ABLATE in the environment cannot change what the shipped kernels compute
 // (the host refuses it too: xylo_hip.cpp do_learn).
 #define XH_ABL(a, k) (XH_DIAG_ABLATE && ((a).ablate & (k)))
+// Phase stamps (trace build, make variant VFLAGS=-DXH_DIAG_TRACE=1, run with
+// XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
+// workgroups records the cycle counter at the 8-wave train kernel's phase
+// boundaries for its first kTraceGroups groups.
+#ifndef XH_DIAG_TRACE
+#define XH_DIAG_TRACE 0
+#endif
+#if XH_DIAG_TRACE
+#define XH_STAMP(a, gi, w, lane, slot)                                        \
+  do {                                                                        \
+    if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups &&      \
+        (lane) == 0)                                                          \
+      (a).trace[((blockIdx.x * kTraceGroups + (gi)) * 8 + (w)) * kTraceSlots + \
+                (slot)] = clock64();                                          \
+  } while (0)
+#else
+#define XH_STAMP(a, gi, w, lane, slot) \
+  do {                                 \
+  } while (0)
+#endif
 
 namespace xh {
-// 1 in the diagnostic build (make diag), 0 in the product library.
-int diag_build() { return XH_DIAG_ABLATE; }
+// 1 in the diagnostic builds (make diag / trace variants), 0 in the product
+// library.
+int diag_build() { return XH_DIAG_ABLATE || XH_DIAG_TRACE; }
 }  // namespace xh
 
 namespace xh {
@@ -331,8 +352,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
-            h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31;
   const int N = a.b.N, t = a.t;
   const int ngroups = N / S::G;
   // forward job of this wave: output tile o2t, r-tiles rt0 .. rt0+FJ-1
@@ -1209,6 +1229,41 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
   }
 }
 
+// 8-wave train kernel schedule knobs (A/B variants, make variant; the
+// defaults are the measured best, tools/gpu_variants.sh):
+//   XH_V_DH1: bit0 fully unroll the dH1 k-loop (64-row groups; the 128-row
+//             kernel spills), bit1 K split by lane half (half h takes
+//             o2 = s + 64h: consecutive steps are adjacent image rows)
+//             config 3: 7.17 -> 7.00 ms unrolled, 6.95 with the split
+//   XH_V_IL:  1 = dH1 interleaved with the first half of dW2 (three
+//             independent MFMA chains), the dW1 VALU work rides in the
+//             second: 7.17 -> 7.23 ms, dropped
+//   XH_V_L3:  1 = the layer-3 weights loaded before the softmax phase
+//             (64-row groups): the layer-3 phase 1070 -> 660 cycles;
+//             XH_V_L3W the same for 128-row groups (15.91 -> 15.82 ms)
+//   measured without the trace stamps, config 3: 7.08 -> 6.67 ms per epoch
+//   (XH_V_DH1 = 1 with XH_V_L3: the same arithmetic, bit-identical)
+//   XH_V_NB3: 1 = no end-of-group barrier (64-row groups): the H1 image
+//             tile is written after the post-forward barrier (layer 1
+//             again, in the MFMA-idle softmax window), so every image
+//             write of group g+1 follows a barrier all waves pass only
+//             after their last image read of group g
+#ifndef XH_V_NB3
+#define XH_V_NB3 0
+#endif
+#ifndef XH_V_DH1
+#define XH_V_DH1 1
+#endif
+#ifndef XH_V_IL
+#define XH_V_IL 0
+#endif
+#ifndef XH_V_L3
+#define XH_V_L3 1
+#endif
+#ifndef XH_V_L3W
+#define XH_V_L3W 1
+#endif
+
 // ================================================ train epoch, 8 waves ====
 // H1 = H2 = 128 (BASELINE configs 3/4/5): 512-thread workgroup = 2 waves per
 // SIMD so one wave's LDS / VALU / barrier time hides behind its partner's
@@ -1371,8 +1426,14 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   };
 
   if (HG == 1 && (int)blockIdx.x < ngroups) fetch_row(blockIdx.x, 0, bv_c, iv_c);
+  constexpr bool kNB3 = XH_V_NB3 && HG == 1;
+  constexpr int kDH1 = HG == 1 ? XH_V_DH1 : 0;
+  constexpr bool kL3 = HG == 1 ? XH_V_L3 : XH_V_L3W;
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int gi = (g - (int)blockIdx.x) / (int)gridDim.x;
+    (void)gi;
+    XH_STAMP(a, gi, w, lane, 0);
     const int gn = g + gridDim.x;
     if (HG == 1 && gn < ngroups) fetch_row(gn, 0, bv_n, iv_n);
     int c_cur;
@@ -1386,18 +1447,27 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
 
     // ---- forward (all R rows) -> per-tile partial logits in LDS
-    f32x16 pre, pre0;
+    f32x16 pre, pre0 = zero16();  // pre0: 128-row groups only
 #pragma unroll
     for (int hg = 0; hg < HG; ++hg) {
       if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
       // the last half-group's H1 image is written here; every half-group's
       // pre-activations stay in registers for the backward
-      pre = forward(hg == HG - 1);
+      pre = forward(hg == HG - 1 && !kNB3);
       if (HG > 1 && hg == 0) pre0 = pre;
       const float zp = logit_part<S, true>(lds, pre, q);
       if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
     }
+    XH_STAMP(a, gi, w, lane, 1);
     __syncthreads();
+    XH_STAMP(a, gi, w, lane, 2);
+    if (kNB3) write_h1_tile();
+    float4 w3v[4];
+    if (kL3) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        w3v[qq] = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
+    }
 
     // ---- logits -> softmax -> loss gradient w.r.t. logits; lane holds the
     // rows lane + 64*k (k < HG)
@@ -1464,6 +1534,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         if (w == 0) accB3 += gz;
       }
     }
+    XH_STAMP(a, gi, w, lane, 3);
 
     // backward, last half-group first: it reuses the forward's registers and
     // H1 image; the earlier half-group keeps its layer-2 pre-activations in
@@ -1485,7 +1556,8 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         const float gr = h == rt ? gzk[hg] : sw;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const float4 ww = lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
+          const float4 ww =
+              kL3 ? w3v[qq] : lds4(lds + S::L_W3 + q * 32 + 8 * qq + 4 * h);
           const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -1498,17 +1570,34 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
           }
         }
       }
+      XH_STAMP(a, gi, w, lane, 4);
       __syncthreads();
+      XH_STAMP(a, gi, w, lane, 5);
 
       // ---- dH1 tile q of r-tile rt (K = H2)
       f32x16 dh = zero16();
-#pragma unroll 16
-      for (int s = 0; s < S::H2 / 2; ++s) {
-        if (XH_ABL(a, 16)) break;
-        const int k = 2 * s + h;
+      constexpr bool kIL = XH_V_IL && HG == 1;
+      auto dh1_step = [&](int s) {
+        const int k = (kDH1 & 2) ? s + (S::H2 / 2) * h : 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
                     DAT[k * S::TS + rt * 32 + lr], dh);
+      };
+      if constexpr (!kIL) {
+        if constexpr (kDH1 & 1) {
+#pragma unroll
+          for (int s = 0; s < S::H2 / 2; ++s) {
+            if (XH_ABL(a, 16)) break;
+            dh1_step(s);
+          }
+        } else {
+#pragma unroll 16
+          for (int s = 0; s < S::H2 / 2; ++s) {
+            if (XH_ABL(a, 16)) break;
+            dh1_step(s);
+          }
+        }
       }
+      XH_STAMP(a, gi, w, lane, 6);
       float xf[S::D];
 #pragma unroll
       for (int f = 0; f < S::D; ++f) xf[f] = feat(f);
@@ -1524,11 +1613,58 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       // The dH1 tile's relu' / dW1 / db1 VALU work rides along, two
       // accumulator registers per 4-row step, in the MFMAs' shadow
       // (7.63 -> 7.44 ms per epoch against running it after dW2).
+      // 128-row groups unroll by 4: 0 B spill (8 B at 8)
+      constexpr int kUnrollW2 = S::HG > 1 ? 4 : 8;
       const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
       const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
-#pragma unroll (S::HG > 1 ? 4 : 8)  // 128-row groups: 0 B spill (8 at 8)
-      for (int s4 = 0; s4 < 8; ++s4) {
+      if constexpr (kIL) {
+        // rows 0..15 of dW2 with all 64 dH1 steps: three independent chains
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const float4 av = lds4(pa + 4 * s4);
+          const float4 b0 = lds4(pb0 + 4 * s4);
+          const float4 b1 = lds4(pb1 + 4 * s4);
+          const float ae[4] = {av.x, av.y, av.z, av.w};
+          const float b0e[4] = {b0.x, b0.y, b0.z, b0.w};
+          const float b1e[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            accW2[0] = mfma32(ae[e], b0e[e], accW2[0]);
+            dh1_step(16 * s4 + 4 * e + 0);
+            dh1_step(16 * s4 + 4 * e + 1);
+            accW2[1] = mfma32(ae[e], b1e[e], accW2[1]);
+            dh1_step(16 * s4 + 4 * e + 2);
+            dh1_step(16 * s4 + 4 * e + 3);
+          }
+        }
+        // rows 16..31 with the dW1 VALU work (4 accumulator registers a step)
+#pragma unroll
+        for (int s4 = 4; s4 < 8; ++s4) {
+          const float4 av = lds4(pa + 4 * s4);
+          const float4 b0 = lds4(pb0 + 4 * s4);
+          const float4 b1 = lds4(pb1 + 4 * s4);
+          accW2[0] = mfma32(av.x, b0.x, accW2[0]);
+          accW2[1] = mfma32(av.x, b1.x, accW2[1]);
+          accW2[0] = mfma32(av.y, b0.y, accW2[0]);
+          accW2[1] = mfma32(av.y, b1.y, accW2[1]);
+          accW2[0] = mfma32(av.z, b0.z, accW2[0]);
+          accW2[1] = mfma32(av.z, b1.z, accW2[1]);
+          accW2[0] = mfma32(av.w, b0.w, accW2[0]);
+          accW2[1] = mfma32(av.w, b1.w, accW2[1]);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * (s4 - 4) + jj;
+            const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
+            sA[j] = fmaf(d, fa, sA[j]);
+            sB[j] = fmaf(d, fb, sB[j]);
+#pragma unroll
+            for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
+          }
+        }
+      }
+#pragma unroll kUnrollW2
+      for (int s4 = 0; s4 < (kIL ? 0 : 8); ++s4) {
         if (XH_ABL(a, 32)) break;
         const float4 av = lds4(pa + 4 * s4);
         const float4 b0 = lds4(pb0 + 4 * s4);
@@ -1557,6 +1693,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
           }
         }
       }
+      XH_STAMP(a, gi, w, lane, 7);
       if constexpr (kMW1) {
         // ---- dW1 / db1 of this half-group by MFMA (see kMW1 above)
         __syncthreads();  // every wave is done with the H1 / dA2 images
@@ -1585,7 +1722,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         }
       }
     }
-    __syncthreads();
+    if (!kNB3) __syncthreads();
     if (HG == 1) {
 #pragma unroll
       for (int d = 0; d < S::D; ++d) {
@@ -1595,6 +1732,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
   }
 
+  if (kNB3) __syncthreads();  // the last group's images read by every wave
   // ---------------------------------------------------- slab write-out ----
   const PolicyLayout L{S::F0, S::H1, S::H2};
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;

@@ -90,7 +90,11 @@ struct PolicyTrainArgs {
   const int *end_list;   // [n_end] t*N + env of terminal transitions
   const int *n_end;      // device scalar
   double *kl_part;       // [gridDim.x] sum over rows of KL(q || p)
+  // diagnostic build only (XH_PHASE_TRACE): per-wave cycle stamps at the
+  // 8-wave train kernel's phase boundaries, [4 blocks][32 groups][8 waves][8]
+  long long *trace;
 };
+constexpr int kTraceBlocks = 4, kTraceGroups = 32, kTraceSlots = 8;
 
 // End-row bookkeeping for KL-PPO (one 1024-thread workgroup).
 struct EndListArgs {

@@ -635,6 +635,18 @@ int do_learn(xh_trainer *t) {
                   "product library (phase ablation exists only in `make "
                   "diag`)", ab);
   }
+  // XH_PHASE_TRACE (diagnostic build): phase stamps of the first epoch's
+  // train launch, summarised on stderr
+  static long long *trace_buf = nullptr;
+  const size_t trace_n = (size_t)xh::kTraceBlocks * xh::kTraceGroups * 8 *
+                         xh::kTraceSlots;
+  if (xh::diag_build() && std::getenv("XH_PHASE_TRACE")) {
+    if (!trace_buf && hipMalloc(&trace_buf, trace_n * 8) != hipSuccess)
+      return fail(XH_ERR_HIP, "trace buffer");
+    if (hipMemsetAsync(trace_buf, 0, trace_n * 8, s) != hipSuccess)
+      return fail(XH_ERR_HIP, "trace buffer");
+    pa.trace = trace_buf;
+  }
   const bool kl = c.algo == XH_KLPPO;
   if (kl) {
     pa.qold = t->qold;
@@ -652,6 +664,35 @@ int do_learn(xh_trainer *t) {
       return xh::launch_policy_train(pa, c.policy_h1, c.policy_h2, t->pslab_n,
                                      s);
     }));
+    if (pa.trace) {
+      std::vector<long long> tr(trace_n);
+      if (hipMemcpyAsync(tr.data(), pa.trace, trace_n * 8,
+                         hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(XH_ERR_HIP, "trace read-back");
+      // per phase: mean cycles over waves and groups 1.. (group 0 warms up);
+      // "group" = stamp 0 of the next group minus stamp 0 of this one
+      double sum[xh::kTraceSlots + 1] = {0};
+      long n = 0;
+      for (int b = 0; b < xh::kTraceBlocks; ++b)
+        for (int gi = 1; gi + 1 < xh::kTraceGroups; ++gi)
+          for (int w = 0; w < 8; ++w) {
+            const long long *p =
+                &tr[((b * xh::kTraceGroups + gi) * 8 + w) * xh::kTraceSlots];
+            const long long *pn = p + 8 * xh::kTraceSlots;
+            if (!p[0] || !pn[0]) continue;
+            for (int k = 1; k < xh::kTraceSlots; ++k) sum[k] += p[k] - p[k - 1];
+            sum[xh::kTraceSlots] += pn[0] - p[xh::kTraceSlots - 1];
+            sum[0] += pn[0] - p[0];
+            ++n;
+          }
+      std::fprintf(stderr, "phase trace (%ld wave-groups, cycles): group %.0f |"
+                   " fwd %.0f bar1 %.0f softmax %.0f layer3 %.0f bar2 %.0f"
+                   " dH1 %.0f dW2 %.0f end+bar3 %.0f\n", n,
+                   sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n, sum[4] / n,
+                   sum[5] / n, sum[6] / n, sum[7] / n, sum[8] / n);
+      pa.trace = nullptr;  // first epoch only
+    }
     CHK(timed(t, "reduce_sgd", [&]() {
       return xh::launch_slab_reduce(t->pslab, t->pslab_n, t->pslab_stride,
                                     t->np, g, s);
