@@ -872,6 +872,19 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
   }
 }
 
+// 4-wave train kernel schedule knobs (A/B variants, make variant), applied
+// to the shapes with one dW2 / dH1 tile per wave (JW = JH = 1: config 2):
+//   XH_V4_UNROLL: bit0 fully unroll the dW2 row loop, bit1 the dH1 loop
+//   XH_V4_L3:     1 = the layer-3 weights loaded before the softmax
+// config 2 (tools/gpu_ab_vars.sh): 0.171 ms per epoch -> 0.169 (bit0),
+// 0.165 (bit1), 0.163 (both), 0.160 (both + L3); same arithmetic order
+#ifndef XH_V4_UNROLL
+#define XH_V4_UNROLL 3
+#endif
+#ifndef XH_V4_L3
+#define XH_V4_L3 1
+#endif
+
 // ============================================================ train epoch ==
 // KL = true: kl_ppo_learner's epoch (policy_gradient.h:310-335) -- every row
 // of the state matrix: transitions, then the open trajectories' end rows
@@ -1018,6 +1031,16 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
     }
     __syncthreads();
 
+    constexpr bool kOne = S::JW == 1 && S::JH == 1 && !KL;  // KL: spills
+    constexpr int kU4 = kOne ? XH_V4_UNROLL : 0;
+    constexpr bool kL34 = kOne && XH_V4_L3;
+    float4 w3v[4];
+    if (kL34) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        w3v[qq] = lds4(lds + S::L_W3 + o2t * 32 + 8 * qq + 4 * h);
+    }
+
     // ---- logits -> softmax -> loss gradient w.r.t. logits (lane = row)
     float gz;
     {
@@ -1072,7 +1095,8 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
         const float gr = wave_shfl(gz, rt * 32 + lr);
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const float4 ww = lds4(lds + S::L_W3 + o2t * 32 + 8 * qq + 4 * h);
+          const float4 ww =
+              kL34 ? w3v[qq] : lds4(lds + S::L_W3 + o2t * 32 + 8 * qq + 4 * h);
           const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -1091,8 +1115,7 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 
     // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows); the JW
     // independent accumulation chains share the dA2 operand
-#pragma unroll 4
-    for (int s = 0; s < (XH_ABL(a, 1) ? 0 : 32); ++s) {
+    auto dw2_step = [&](int s) {
       const int r = 2 * s + h;
       const float av = DAimg[r * S::AS + o2t * 32 + lr];
 #pragma unroll
@@ -1101,6 +1124,13 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
         if (NOT >= 4 || it < NIT)
           accW2[q] = mfma32(av, H1img[r * S::HS + it * 32 + lr], accW2[q]);
       }
+    };
+    if constexpr (kU4 & 1) {
+#pragma unroll
+      for (int s = 0; s < 32; ++s) dw2_step(s);
+    } else {
+#pragma unroll 4
+      for (int s = 0; s < (XH_ABL(a, 1) ? 0 : 32); ++s) dw2_step(s);
     }
 
     // ---- dH1^T[i][r] = sum_o2 W2[o2][i] dA2[r][o2]; relu'; dW1, db1
@@ -1108,8 +1138,7 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
       f32x16 dh[S::JH];
 #pragma unroll
       for (int q = 0; q < S::JH; ++q) dh[q] = zero16();
-#pragma unroll 4
-      for (int s = 0; s < (XH_ABL(a, 2) ? 0 : S::H2 / 2); ++s) {
+      auto dh1_step = [&](int s) {
         const int k = 2 * s + h;
         const float av = lds[S::L_W2 + k * S::W2S + it_own * 32 + lr];
 #pragma unroll
@@ -1118,6 +1147,13 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
           if (NIT >= 4 || rt < 2)
             dh[q] = mfma32(av, DAimg[(rt * 32 + lr) * S::AS + k], dh[q]);
         }
+      };
+      if constexpr (kU4 & 2) {
+#pragma unroll
+        for (int s = 0; s < S::H2 / 2; ++s) dh1_step(s);
+      } else {
+#pragma unroll 4
+        for (int s = 0; s < (XH_ABL(a, 2) ? 0 : S::H2 / 2); ++s) dh1_step(s);
       }
 #pragma unroll
       for (int q = 0; q < S::JH; ++q) {

@@ -168,6 +168,7 @@ struct xh_trainer {
   bool timing = false;
   bool counted = false;  // holds a reference on ctx
   std::vector<timed_event> events;
+  std::vector<hipEvent_t> event_pool;  // recycled by reset_timing
   std::vector<void *> allocs;
 
   xh::Batch batch() const {
@@ -239,6 +240,18 @@ int dalloc(xh_trainer *t, P **p, size_t bytes) {
   return XH_OK;
 }
 
+// Timing events come from a pool (reset_timing returns them), without the
+// system-scope fence: they only time launches, every host read of device
+// memory synchronises the stream itself.
+hipError_t pooled_event(xh_trainer *t, hipEvent_t *e) {
+  if (!t->event_pool.empty()) {
+    *e = t->event_pool.back();
+    t->event_pool.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreateWithFlags(e, hipEventDisableSystemFence);
+}
+
 // Launch wrapper: optional HIP-event timing on the trainer's stream.
 template <class F>
 int timed(xh_trainer *t, const char *name, F &&launch) {
@@ -246,8 +259,8 @@ int timed(xh_trainer *t, const char *name, F &&launch) {
   timed_event ev;
   if (t->timing) {
     ev.name = name;
-    HIPCHK(hipEventCreate(&ev.start));
-    HIPCHK(hipEventCreate(&ev.stop));
+    HIPCHK(pooled_event(t, &ev.start));
+    HIPCHK(pooled_event(t, &ev.stop));
     HIPCHK(hipEventRecord(ev.start, s));
   }
   hipError_t e = launch();
@@ -1269,6 +1282,7 @@ int xh_trainer_destroy(xh_trainer *t) {
       (void)hipEventDestroy(ev.start);
       (void)hipEventDestroy(ev.stop);
     }
+    for (hipEvent_t e : t->event_pool) (void)hipEventDestroy(e);
     for (void *p : t->allocs) (void)hipFree(p);
     if (t->pg.host_active) (void)hipHostFree(t->pg.host_active);
     xh_ctx *c = t->ctx;
@@ -1537,8 +1551,8 @@ int xh_trainer_reset_timing(xh_trainer *t) {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     for (auto &ev : t->events) {
-      (void)hipEventDestroy(ev.start);
-      (void)hipEventDestroy(ev.stop);
+      t->event_pool.push_back(ev.start);
+      t->event_pool.push_back(ev.stop);
     }
     t->events.clear();
     return XH_OK;
