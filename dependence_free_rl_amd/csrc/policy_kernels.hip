@@ -1287,6 +1287,15 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 #ifndef XH_V_NB3
 #define XH_V_NB3 0
 #endif
+//   XH_V_DH1E: 1 = dH1's K slice of the wave's own H2 tile issued from the
+//             layer-3 registers before the barrier (64-row groups)
+#ifndef XH_V_DH1E
+#define XH_V_DH1E 0
+#endif
+//   XH_V_DH1W: the dH1 loop's unroll factor in the 128-row kernel
+#ifndef XH_V_DH1W
+#define XH_V_DH1W 16
+#endif
 #ifndef XH_V_DH1
 #define XH_V_DH1 1
 #endif
@@ -1585,6 +1594,11 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         write_h1_tile();  // the H1 image again (layer 1 only)
         pre = pre0;       // layer 2 kept from the forward
       }
+      // dH1 tile q of r-tile rt (K = H2); kE: its K slice o2 in H2 tile q
+      // from the layer-3 registers before the barrier (MFMAs in the serial
+      // window), the other three slices from the image after it
+      f32x16 dh = zero16();
+      constexpr bool kE = XH_V_DH1E && HG == 1;
       // ---- backward through layer 3 and the layer-2 relu
       {
         // row rt*32 + lr's gradient: own lane in half rt, else lane ^ 32
@@ -1603,6 +1617,10 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
             const float d = v > 0.0f ? gr * wq[u] : 0.0f;
             if (!kB2Late) accB2[j] += d;
             DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
+            if (kE)
+              dh = mfma32(lds[S::L_W2 + (q * 32 + acc_row(j, h)) * S::W2S +
+                              q * 32 + lr],
+                          d, dh);
           }
         }
       }
@@ -1610,15 +1628,24 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       __syncthreads();
       XH_STAMP(a, gi, w, lane, 5);
 
-      // ---- dH1 tile q of r-tile rt (K = H2)
-      f32x16 dh = zero16();
       constexpr bool kIL = XH_V_IL && HG == 1;
       auto dh1_step = [&](int s) {
         const int k = (kDH1 & 2) ? s + (S::H2 / 2) * h : 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
                     DAT[k * S::TS + rt * 32 + lr], dh);
       };
-      if constexpr (!kIL) {
+      if constexpr (kE) {
+#pragma unroll
+        for (int u = 1; u < 4; ++u) {
+          const int tb = ((q + u) & 3) * 32;  // wave-uniform H2 tile base
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) {
+            const int k = tb + 2 * s2 + h;
+            dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
+                        DAT[k * S::TS + rt * 32 + lr], dh);
+          }
+        }
+      } else if constexpr (!kIL) {
         if constexpr (kDH1 & 1) {
 #pragma unroll
           for (int s = 0; s < S::H2 / 2; ++s) {
@@ -1626,7 +1653,8 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
             dh1_step(s);
           }
         } else {
-#pragma unroll 16
+          constexpr int kU = XH_V_DH1W;  // 128-row groups
+#pragma unroll kU
           for (int s = 0; s < S::H2 / 2; ++s) {
             if (XH_ABL(a, 16)) break;
             dh1_step(s);
