@@ -395,6 +395,94 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
   }
 }
 
+// Partial logits of one 64-row half-group for the wave-per-env rollouts,
+// one 32-row r-tile at a time (XH_V_RPASS): the wave keeps all four H2
+// tiles' accumulators of the r-tile (four independent MFMA chains) and
+// computes each layer-1 tile once per r-tile instead of once per H2 tile
+// (config 3: 576 -> 528 MFMAs per env; config 5: 1216 -> 1072).  Every
+// sum runs in the order of the tile-major loop (layer 1 over k-steps, + bias,
+// relu; layer 2 over it, q, u; + bias; the logit over o2t), so logits are
+// bit-identical.  zl[rt]: the partial logit of row rt*32 + (lane & 31).
+// Measured (tools/gpu_ab_vars.sh): config 3 rollout 2.44 -> 2.19 ms per
+// iteration, config 5 5.09 -> 4.83 ms, at 12 waves per workgroup (3 per SIMD;
+// 4 per SIMD spills at 128 VGPRs, and without the scheduling barriers the
+// operand reads of all four tiles are hoisted: 428 B of spills).
+#ifndef XH_V_RPASS
+#define XH_V_RPASS 1
+#endif
+// waves per workgroup of the wave-per-env rollouts (one workgroup of 12 per
+// CU = 3 waves per SIMD with 168 VGPRs: the r-tile pass keeps four H2 tiles'
+// accumulators; 8 = two workgroups per CU, 4 waves per SIMD, 128 VGPRs)
+#ifndef XH_V_RWAVES
+#define XH_V_RWAVES (XH_V_RPASS ? 12 : 8)
+#endif
+constexpr int kRollWaves = XH_V_RWAVES;
+#ifndef XH_V_RSB
+#define XH_V_RSB 1
+#endif
+constexpr int kRollOcc = kRollWaves == 8 ? 4 : (kRollWaves == 12 ? 3 : 2);
+template <class S>
+__device__ __forceinline__ void wave_logits_rpass(const float *lds,
+                                                  const RowRaw<S> &cur,
+                                                  float (&zl)[2]) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    float xb[S::S1];
+#pragma unroll
+    for (int s = 0; s < S::S1; ++s) xb[s] = row_feature<S>(cur, rt, 2 * s + h);
+    f32x16 pre[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) pre[o] = zero16();
+#pragma unroll 1
+    for (int it = 0; it < 4; ++it) {
+      f32x16 t1 = zero16();
+#pragma unroll
+      for (int s = 0; s < S::S1; ++s) {
+        const int k = 2 * s + h;
+        const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+        t1 = mfma32(wa, xb[s], t1);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * q + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t1[4 * q + u] = relu(t1[4 * q + u] + bq[u]);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const float *wrow = lds + S::L_W2 + (o * 32 + lr) * S::W2S + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 a4 = lds4(wrow + it * 32 + 8 * q);
+          const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) pre[o] = mfma32(av[u], t1[4 * q + u], pre[o]);
+        }
+        // keep the scheduler from hoisting every tile's operand reads
+        if (XH_V_RSB) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    float z = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = lds4(lds + S::L_B2 + o * 32 + 8 * q + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pre[o][4 * q + u] += bq[u];
+      }
+      z += logit_part<S>(lds, pre[o], o);
+    }
+    if (rt == 0)
+      zl[0] = z;
+    else
+      zl[1] = z;
+  }
+}
+
 // ================================================ rollout step, wave per env ==
 // B = 64, [128,128] (config 3): one wave per env.  The wave runs all four H2
 // tiles itself (layer 1 recomputed per tile, as each of rollout_step_kernel's
@@ -405,7 +493,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
 // rollout_step_kernel (layer1, layer2, logit_part, the o-ordered logit sum),
 // so logits, probabilities and actions are bit-identical.
 template <class S>
-__global__ __launch_bounds__(512, 4) void rollout_wave_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave_kernel(RolloutArgs a) {
   static_assert(S::B == 64 && S::NIT == 4 && S::NOT == 4, "wave rollout: B=64, [128,128]");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
@@ -422,8 +510,9 @@ __global__ __launch_bounds__(512, 4) void rollout_wave_kernel(RolloutArgs a) {
 #pragma unroll
       for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
     float zl[2] = {0.0f, 0.0f};  // partial logit sums of rows lr / 32 + lr
+    if (XH_V_RPASS) wave_logits_rpass<S>(lds, cur, zl);
 #pragma unroll 1
-    for (int o2t = 0; o2t < 4; ++o2t) {
+    for (int o2t = 0; o2t < (XH_V_RPASS ? 0 : 4); ++o2t) {
       const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
       f32x16 pre[2];
       pre[0] = zero16();
@@ -649,7 +738,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step128_kernel(RolloutArgs a) 
 // forward and the sampler and four waves per SIMD to hide the
 // double-precision sampler under the other waves' MFMAs.
 template <class S>
-__global__ __launch_bounds__(512, 4) void rollout_wave128_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave128_kernel(RolloutArgs a) {
   static_assert(S::B == 128 && S::NIT == 4 && S::NOT == 4,
                 "wave rollout: B=128, [128,128]");
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -682,8 +771,9 @@ __global__ __launch_bounds__(512, 4) void rollout_wave128_kernel(RolloutArgs a) 
 #pragma unroll
         for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
       float zl[2] = {0.0f, 0.0f};
+      if (XH_V_RPASS) wave_logits_rpass<S>(lds, cur, zl);
 #pragma unroll 1
-      for (int o2t = 0; o2t < 4; ++o2t) {
+      for (int o2t = 0; o2t < (XH_V_RPASS ? 0 : 4); ++o2t) {
         const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
         f32x16 pre[2];
         pre[0] = zero16();
@@ -1981,9 +2071,10 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                     (int)rollout_lds<S>());                  \
           wattr = true;                                                      \
         }                                                                    \
-        const int wg = (a.b.N + 7) / 8;                                      \
+        const int wg = (a.b.N + kRollWaves - 1) / kRollWaves;                \
+        const int wgr = kRollWaves == 8 ? grid : cu_count();                 \
         hipLaunchKernelGGL(rollout_wave128_kernel<S>,                        \
-                           dim3(grid < wg ? grid : wg), dim3(512),           \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRollWaves), \
                            rollout_lds<S>(), s, a);                          \
         return hipGetLastError();                                            \
       }                                                                      \
@@ -1997,9 +2088,10 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                     (int)rollout_lds<S>());                  \
           wattr = true;                                                      \
         }                                                                    \
-        const int wg = (ng + 7) / 8;                                         \
+        const int wg = (ng + kRollWaves - 1) / kRollWaves;                   \
+        const int wgr = kRollWaves == 8 ? grid : cu_count();                 \
         hipLaunchKernelGGL(rollout_wave_kernel<S>,                           \
-                           dim3(grid < wg ? grid : wg), dim3(512),           \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRollWaves), \
                            rollout_lds<S>(), s, a);                          \
         return hipGetLastError();                                            \
       }                                                                      \
