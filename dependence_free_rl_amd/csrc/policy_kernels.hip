@@ -1356,41 +1356,22 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 }
 
 // 8-wave train kernel schedule knobs (A/B variants, make variant; the
-// defaults are the measured best, tools/gpu_variants.sh):
+// defaults are the measured best, tools/gpu_ab_vars.sh; the dropped variants
+// are listed in DESIGN.md §8):
 //   XH_V_DH1: bit0 fully unroll the dH1 k-loop (64-row groups; the 128-row
 //             kernel spills), bit1 K split by lane half (half h takes
 //             o2 = s + 64h: consecutive steps are adjacent image rows)
-//             config 3: 7.17 -> 7.00 ms unrolled, 6.95 with the split
-//   XH_V_IL:  1 = dH1 interleaved with the first half of dW2 (three
-//             independent MFMA chains), the dW1 VALU work rides in the
-//             second: 7.17 -> 7.23 ms, dropped
+//   XH_V_DH1W: the dH1 loop's unroll factor in the 128-row kernel
 //   XH_V_L3:  1 = the layer-3 weights loaded before the softmax phase
 //             (64-row groups): the layer-3 phase 1070 -> 660 cycles;
 //             XH_V_L3W the same for 128-row groups (15.91 -> 15.82 ms)
 //   measured without the trace stamps, config 3: 7.08 -> 6.67 ms per epoch
 //   (XH_V_DH1 = 1 with XH_V_L3: the same arithmetic, bit-identical)
-//   XH_V_NB3: 1 = no end-of-group barrier (64-row groups): the H1 image
-//             tile is written after the post-forward barrier (layer 1
-//             again, in the MFMA-idle softmax window), so every image
-//             write of group g+1 follows a barrier all waves pass only
-//             after their last image read of group g
-#ifndef XH_V_NB3
-#define XH_V_NB3 0
-#endif
-//   XH_V_DH1E: 1 = dH1's K slice of the wave's own H2 tile issued from the
-//             layer-3 registers before the barrier (64-row groups)
-#ifndef XH_V_DH1E
-#define XH_V_DH1E 0
-#endif
-//   XH_V_DH1W: the dH1 loop's unroll factor in the 128-row kernel
-#ifndef XH_V_DH1W
-#define XH_V_DH1W 16
-#endif
 #ifndef XH_V_DH1
 #define XH_V_DH1 1
 #endif
-#ifndef XH_V_IL
-#define XH_V_IL 0
+#ifndef XH_V_DH1W
+#define XH_V_DH1W 16
 #endif
 #ifndef XH_V_L3
 #define XH_V_L3 1
@@ -1496,23 +1477,28 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
 #pragma unroll
     for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
     const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      f32x16 t1;
+    // layer-1 tile it's MFMA chain (from its biases)
+    auto l1 = [&](int it) {
+      f32x16 t;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const float4 bb = lds4(lds + S::L_B1 + it * 32 + 8 * qq + 4 * h);
-        t1[4 * qq + 0] = bb.x;
-        t1[4 * qq + 1] = bb.y;
-        t1[4 * qq + 2] = bb.z;
-        t1[4 * qq + 3] = bb.w;
+        t[4 * qq + 0] = bb.x;
+        t[4 * qq + 1] = bb.y;
+        t[4 * qq + 2] = bb.z;
+        t[4 * qq + 3] = bb.w;
       }
 #pragma unroll
       for (int s = 0; s < S::S1; ++s) {
         const int k = 2 * s + h;
         const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
-        t1 = mfma32(wa, xb[s], t1);
+        t = mfma32(wa, xb[s], t);
       }
+      return t;
+    };
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      f32x16 t1 = l1(it);
 #pragma unroll
       for (int j = 0; j < 16; ++j) t1[j] = relu(t1[j]);
       if (write_h1 && it == q) {
@@ -1561,7 +1547,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   };
 
   if (HG == 1 && (int)blockIdx.x < ngroups) fetch_row(blockIdx.x, 0, bv_c, iv_c);
-  constexpr bool kNB3 = XH_V_NB3 && HG == 1;
   constexpr int kDH1 = HG == 1 ? XH_V_DH1 : 0;
   constexpr bool kL3 = HG == 1 ? XH_V_L3 : XH_V_L3W;
 
@@ -1588,7 +1573,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
       // the last half-group's H1 image is written here; every half-group's
       // pre-activations stay in registers for the backward
-      pre = forward(hg == HG - 1 && !kNB3);
+      pre = forward(hg == HG - 1);
       if (HG > 1 && hg == 0) pre0 = pre;
       const float zp = logit_part<S, true>(lds, pre, q);
       if (lane < 32) lds[S::L_Z + q * R + hg * 64 + rt * 32 + lr] = zp;
@@ -1596,7 +1581,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     XH_STAMP(a, gi, w, lane, 1);
     __syncthreads();
     XH_STAMP(a, gi, w, lane, 2);
-    if (kNB3) write_h1_tile();
     float4 w3v[4];
     if (kL3) {
 #pragma unroll
@@ -1684,11 +1668,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         write_h1_tile();  // the H1 image again (layer 1 only)
         pre = pre0;       // layer 2 kept from the forward
       }
-      // dH1 tile q of r-tile rt (K = H2); kE: its K slice o2 in H2 tile q
-      // from the layer-3 registers before the barrier (MFMAs in the serial
-      // window), the other three slices from the image after it
-      f32x16 dh = zero16();
-      constexpr bool kE = XH_V_DH1E && HG == 1;
       // ---- backward through layer 3 and the layer-2 relu
       {
         // row rt*32 + lr's gradient: own lane in half rt, else lane ^ 32
@@ -1707,10 +1686,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
             const float d = v > 0.0f ? gr * wq[u] : 0.0f;
             if (!kB2Late) accB2[j] += d;
             DAT[(q * 32 + acc_row(j, h)) * S::TS + rt * 32 + lr] = d;
-            if (kE)
-              dh = mfma32(lds[S::L_W2 + (q * 32 + acc_row(j, h)) * S::W2S +
-                              q * 32 + lr],
-                          d, dh);
           }
         }
       }
@@ -1718,37 +1693,25 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       __syncthreads();
       XH_STAMP(a, gi, w, lane, 5);
 
-      constexpr bool kIL = XH_V_IL && HG == 1;
+      // ---- dH1 tile q of r-tile rt (K = H2)
+      f32x16 dh = zero16();
       auto dh1_step = [&](int s) {
         const int k = (kDH1 & 2) ? s + (S::H2 / 2) * h : 2 * s + h;
         dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
                     DAT[k * S::TS + rt * 32 + lr], dh);
       };
-      if constexpr (kE) {
+      if constexpr (kDH1 & 1) {
 #pragma unroll
-        for (int u = 1; u < 4; ++u) {
-          const int tb = ((q + u) & 3) * 32;  // wave-uniform H2 tile base
-#pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2) {
-            const int k = tb + 2 * s2 + h;
-            dh = mfma32(lds[S::L_W2 + k * S::W2S + q * 32 + lr],
-                        DAT[k * S::TS + rt * 32 + lr], dh);
-          }
+        for (int s = 0; s < S::H2 / 2; ++s) {
+          if (XH_ABL(a, 16)) break;
+          dh1_step(s);
         }
-      } else if constexpr (!kIL) {
-        if constexpr (kDH1 & 1) {
-#pragma unroll
-          for (int s = 0; s < S::H2 / 2; ++s) {
-            if (XH_ABL(a, 16)) break;
-            dh1_step(s);
-          }
-        } else {
-          constexpr int kU = XH_V_DH1W;  // 128-row groups
+      } else {
+        constexpr int kU = XH_V_DH1W;  // 128-row groups
 #pragma unroll kU
-          for (int s = 0; s < S::H2 / 2; ++s) {
-            if (XH_ABL(a, 16)) break;
-            dh1_step(s);
-          }
+        for (int s = 0; s < S::H2 / 2; ++s) {
+          if (XH_ABL(a, 16)) break;
+          dh1_step(s);
         }
       }
       XH_STAMP(a, gi, w, lane, 6);
@@ -1772,53 +1735,8 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
       const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
-      if constexpr (kIL) {
-        // rows 0..15 of dW2 with all 64 dH1 steps: three independent chains
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const float4 av = lds4(pa + 4 * s4);
-          const float4 b0 = lds4(pb0 + 4 * s4);
-          const float4 b1 = lds4(pb1 + 4 * s4);
-          const float ae[4] = {av.x, av.y, av.z, av.w};
-          const float b0e[4] = {b0.x, b0.y, b0.z, b0.w};
-          const float b1e[4] = {b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            accW2[0] = mfma32(ae[e], b0e[e], accW2[0]);
-            dh1_step(16 * s4 + 4 * e + 0);
-            dh1_step(16 * s4 + 4 * e + 1);
-            accW2[1] = mfma32(ae[e], b1e[e], accW2[1]);
-            dh1_step(16 * s4 + 4 * e + 2);
-            dh1_step(16 * s4 + 4 * e + 3);
-          }
-        }
-        // rows 16..31 with the dW1 VALU work (4 accumulator registers a step)
-#pragma unroll
-        for (int s4 = 4; s4 < 8; ++s4) {
-          const float4 av = lds4(pa + 4 * s4);
-          const float4 b0 = lds4(pb0 + 4 * s4);
-          const float4 b1 = lds4(pb1 + 4 * s4);
-          accW2[0] = mfma32(av.x, b0.x, accW2[0]);
-          accW2[1] = mfma32(av.x, b1.x, accW2[1]);
-          accW2[0] = mfma32(av.y, b0.y, accW2[0]);
-          accW2[1] = mfma32(av.y, b1.y, accW2[1]);
-          accW2[0] = mfma32(av.z, b0.z, accW2[0]);
-          accW2[1] = mfma32(av.z, b1.z, accW2[1]);
-          accW2[0] = mfma32(av.w, b0.w, accW2[0]);
-          accW2[1] = mfma32(av.w, b1.w, accW2[1]);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int j = 4 * (s4 - 4) + jj;
-            const float d = hcol[acc_row(j, h) * S::TS] > 0.0f ? dh[j] : 0.0f;
-            sA[j] = fmaf(d, fa, sA[j]);
-            sB[j] = fmaf(d, fb, sB[j]);
-#pragma unroll
-            for (int f = 0; f < S::D; ++f) accW1[j][f] += d * xf[f];
-          }
-        }
-      }
 #pragma unroll kUnrollW2
-      for (int s4 = 0; s4 < (kIL ? 0 : 8); ++s4) {
+      for (int s4 = 0; s4 < 8; ++s4) {
         if (XH_ABL(a, 32)) break;
         const float4 av = lds4(pa + 4 * s4);
         const float4 b0 = lds4(pb0 + 4 * s4);
@@ -1876,7 +1794,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         }
       }
     }
-    if (!kNB3) __syncthreads();
+    __syncthreads();
     if (HG == 1) {
 #pragma unroll
       for (int d = 0; d < S::D; ++d) {
@@ -1886,7 +1804,6 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
   }
 
-  if (kNB3) __syncthreads();  // the last group's images read by every wave
   // ---------------------------------------------------- slab write-out ----
   const PolicyLayout L{S::F0, S::H1, S::H2};
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
