@@ -109,16 +109,14 @@ __global__ void adv_normalize_kernel(float *adv, long n, const double *stats,
     adv[i] = (float)(((double)adv[i] - mean) * inv);
 }
 
-// Deterministic slab reduction: out[i] = sum over slabs in a fixed order.
+// Deterministic slab reduction: the sum over slabs in a fixed order.
 // A 256-thread block takes 64 consecutive entries x 4 slab ranges (each
 // wave reads 256-byte rows, enough blocks to cover the chip); the 4 range
-// sums combine in LDS as (s0 + s1) + (s2 + s3).
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
-                                                          int nslab, int stride,
-                                                          int n, float *out) {
+// sums combine in LDS as (s0 + s1) + (s2 + s3).  Returned to wave 0's lanes.
+__device__ __forceinline__ float slab_sum(const float *slab, int nslab,
+                                          int stride, int n, int i) {
   __shared__ float part[4][64];
   const int p = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + p;
   const int per = (nslab + 3) / 4, k0 = r * per,
             k1 = k0 + per < nslab ? k0 + per : nslab;
   float s = 0.0f;
@@ -128,8 +126,41 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
   }
   part[r][p] = s;
   __syncthreads();
-  if (r == 0 && i < n)
-    out[i] = (part[0][p] + part[1][p]) + (part[2][p] + part[3][p]);
+  return (part[0][p] + part[1][p]) + (part[2][p] + part[3][p]);
+}
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
+                                                          int nslab, int stride,
+                                                          int n, float *out) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float g = slab_sum(slab, nslab, stride, n, i);
+  if (threadIdx.x < 64 && i < n) out[i] = g;
+}
+
+// One parameter's update, the reference's operation order:
+//   sgd_optimizer::next_parameters (nn.h:622-625): p * (1 - wd) - g * lr
+//   momentum_optimizer::next_parameters (nn.h:637-651): v = rho v + g;
+//     p - v * lr
+//   adam_optimizer::next_parameters (nn.h:666-691): m, v moments,
+//     bias-corrected by c1 = 1 - beta1^t, c2 = 1 - beta2^t;
+//     p - m^ lr / (sqrt(v^) + 1e-7)
+__device__ __forceinline__ void opt_update(float *p, float *m, float *v, int i,
+                                           float gi, const OptStep &o) {
+#pragma clang fp contract(off)
+  if (o.kind == 0) {
+    p[i] = p[i] * (1.0f - o.wd) - gi * o.lr;
+  } else if (o.kind == 1) {
+    const float vel = 0.9f * m[i] + gi;
+    m[i] = vel;
+    p[i] = p[i] - vel * o.lr;
+  } else {
+    const float m1 = m[i] * o.beta1 + gi * (1.0f - o.beta1);
+    const float m2 = v[i] * o.beta2 + gi * gi * (1.0f - o.beta2);
+    m[i] = m1;
+    v[i] = m2;
+    const float mu = m1 / o.c1, vu = m2 / o.c2;
+    p[i] = p[i] - mu * o.lr / (sqrtf(vu) + 1e-7f);
+  }
 }
 
 // sgd_optimizer::next_parameters (nn.h:622-625): p * (1 - wd) - g * lr
@@ -142,28 +173,24 @@ __global__ void sgd_kernel(float *p, const float *g, int n, float lr,
     p[i] = p[i] * keep - g[i] * lr;
 }
 
-// momentum_optimizer::next_parameters (nn.h:637-651): v = rho v + g;
-// p - v * lr.  adam_optimizer::next_parameters (nn.h:666-691): m, v moments,
-// bias-corrected by c1 = 1 - beta1^t, c2 = 1 - beta2^t; p - m^ lr /
-// (sqrt(v^) + 1e-7).  One element per lane, the reference's operation order.
+// momentum / adam steps (opt_update), one element per lane
 __global__ void opt_kernel(float *p, const float *g, float *m, float *v, int n,
                            OptStep o) {
-#pragma clang fp contract(off)
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    if (o.kind == 1) {
-      const float vel = 0.9f * m[i] + gi;
-      m[i] = vel;
-      p[i] = p[i] - vel * o.lr;
-    } else {
-      const float m1 = m[i] * o.beta1 + gi * (1.0f - o.beta1);
-      const float m2 = v[i] * o.beta2 + gi * gi * (1.0f - o.beta2);
-      m[i] = m1;
-      v[i] = m2;
-      const float mu = m1 / o.c1, vu = m2 / o.c2;
-      p[i] = p[i] - mu * o.lr / (sqrtf(vu) + 1e-7f);
-    }
+       i += gridDim.x * blockDim.x)
+    opt_update(p, m, v, i, g[i], o);
+}
+
+// Single rank: the slab reduce and the optimizer step in one launch (the
+// reduced gradient is still written out for introspection).
+__global__ __launch_bounds__(256) void slab_reduce_opt_kernel(
+    const float *slab, int nslab, int stride, int n, float *out, float *p,
+    float *m, float *v, OptStep o) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float g = slab_sum(slab, nslab, stride, n, i);
+  if (threadIdx.x < 64 && i < n) {
+    out[i] = g;
+    opt_update(p, m, v, i, g, o);
   }
 }
 
@@ -211,6 +238,14 @@ hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s) {
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, s,
                      slab, nslab, stride, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
+                                  int n, float *out, float *params, float *m,
+                                  float *v, OptStep o, hipStream_t s) {
+  hipLaunchKernelGGL(slab_reduce_opt_kernel, dim3((n + 63) / 64), dim3(256), 0,
+                     s, slab, nslab, stride, n, out, params, m, v, o);
   return hipGetLastError();
 }
 

@@ -298,10 +298,16 @@ hipError_t launch_sgd(float *params, const float *grad, int n, float lr,
 // m (velocity / first moment) and v (second moment); c1, c2 = adam's bias
 // corrections 1 - beta^t computed on the host as the reference does.
 struct OptStep {
-  int kind;
+  int kind;  // XH_OPT_SGD / XH_OPT_MOMENTUM / XH_OPT_ADAM
   float lr, beta1, beta2, c1, c2;
+  float wd;  // sgd weight decay
 };
 hipError_t launch_opt(float *params, const float *grad, float *m, float *v,
                       int n, OptStep o, hipStream_t s);
+// Single-rank fusion of launch_slab_reduce and the optimizer step: the same
+// fixed-order slab sum (written to out) and the same per-element update.
+hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
+                                  int n, float *out, float *params, float *m,
+                                  float *v, OptStep o, hipStream_t s);
 
 }  // namespace xh

@@ -475,9 +475,8 @@ int eval_common(xh_ctx *ctx, const xh::EnvDesc &env, int G, xh_eval *e,
 }
 
 // optimizer::step's next_parameters for net `which` (nn.h:594-698).
-int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
-              int n) {
-  hipStream_t s = t->ctx->stream;
+// The optimizer step's scalars (advances adam's step counter).
+xh::OptStep opt_step(xh_trainer *t, int which) {
   auto &o = t->opt[which];
   // lr_scale_rows (opt-in): lr / rows of the job instead of the raw lr on
   // the row-summed gradient (nn.h:94-98, 624)
@@ -485,19 +484,47 @@ int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
                        ? (float)((double)o.lr /
                                  ((double)t->T() * t->cfg.num_envs_global))
                        : o.lr;
-  if (o.kind == XH_OPT_SGD)
-    return timed(t, "reduce_sgd", [&]() {
-      return xh::launch_sgd(params, grad, n, lr, o.wd, s);
-    });
-  xh::OptStep st{o.kind, lr, o.beta1, o.beta2, 1.0f, 1.0f};
+  xh::OptStep st{o.kind, lr, o.beta1, o.beta2, 1.0f, 1.0f, o.wd};
   if (o.kind == XH_OPT_ADAM) {  // host float powf, as the reference
     st.c1 = 1 - powf(o.beta1, o.t);
     st.c2 = 1 - powf(o.beta2, o.t);
     o.t += 1;
   }
+  return st;
+}
+
+int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
+              int n) {
+  hipStream_t s = t->ctx->stream;
+  auto &o = t->opt[which];
+  const xh::OptStep st = opt_step(t, which);
+  if (o.kind == XH_OPT_SGD)
+    return timed(t, "reduce_sgd", [&]() {
+      return xh::launch_sgd(params, grad, n, st.lr, st.wd, s);
+    });
   return timed(t, "reduce_sgd", [&]() {
     return xh::launch_opt(params, grad, o.m, o.v, n, st, s);
   });
+}
+
+// Slab reduce -> (all-reduce) -> optimizer step.  One rank: one fused launch
+// (the same sums and updates); more ranks: the all-reduce sits between.
+int reduce_and_step(xh_trainer *t, int which, const float *slab, int nslab,
+                    int stride, int n, float *grad, float *params) {
+  hipStream_t s = t->ctx->stream;
+  if (!t->ctx->comm) {
+    auto &o = t->opt[which];
+    const xh::OptStep st = opt_step(t, which);
+    return timed(t, "reduce_sgd", [&]() {
+      return xh::launch_slab_reduce_opt(slab, nslab, stride, n, grad, params,
+                                        o.m, o.v, st, s);
+    });
+  }
+  CHK(timed(t, "reduce_sgd", [&]() {
+    return xh::launch_slab_reduce(slab, nslab, stride, n, grad, s);
+  }));
+  CHK(allreduce(t, grad, n));
+  return opt_apply(t, which, params, grad, n);
 }
 
 int do_pg_rollout(xh_trainer *t);
@@ -599,12 +626,8 @@ int do_learn(xh_trainer *t) {
   CHK(timed(t, "value", [&]() {
     return xh::mlp_backward(vm, t->vslab, t->vslab_stride, t->vslab_n, s);
   }));
-  CHK(timed(t, "reduce_sgd", [&]() {
-    return xh::launch_slab_reduce(t->vslab, t->vslab_n, t->vslab_stride, t->nv,
-                                  t->vgrad, s);
-  }));
-  CHK(allreduce(t, t->vgrad, t->nv));
-  CHK(opt_apply(t, XH_VALUE, t->vp, t->vgrad, t->nv));
+  CHK(reduce_and_step(t, XH_VALUE, t->vslab, t->vslab_n, t->vslab_stride,
+                      t->nv, t->vgrad, t->vp));
   // calculate_advantage (policy_gradient.h:220-281) on post-update values;
   // GAE zeroes V(terminal), the targets above used V(E_t)
   vm.max_rows = NS;
@@ -706,11 +729,9 @@ int do_learn(xh_trainer *t) {
                    sum[5] / n, sum[6] / n, sum[7] / n, sum[8] / n);
       pa.trace = nullptr;  // first epoch only
     }
-    CHK(timed(t, "reduce_sgd", [&]() {
-      return xh::launch_slab_reduce(t->pslab, t->pslab_n, t->pslab_stride,
-                                    t->np, g, s);
-    }));
-    CHK(allreduce(t, g, t->np));
+    // the optimizer step does not read beta: it may precede the KL update
+    CHK(reduce_and_step(t, XH_POLICY, t->pslab, t->pslab_n, t->pslab_stride,
+                        t->np, g, t->pp));
     if (kl) {  // mean KL over the job's rows -> beta for the next epoch
       CHK(timed(t, "kl", [&]() {
         return xh::launch_kl_reduce(t->kl_part, t->pslab_n, t->n_end,
@@ -723,7 +744,6 @@ int do_learn(xh_trainer *t) {
                                          t->kl_log + 3 * e, s);
       }));
     }
-    CHK(opt_apply(t, XH_POLICY, t->pp, g, t->np));
   }
   t->need_shift = true;
   return XH_OK;
@@ -947,12 +967,8 @@ int do_pg_learn(xh_trainer *t) {
   CHK(timed(t, "policy_train", [&]() {
     return xh::mlp_backward(m, t->pslab, t->pslab_stride, t->pslab_n, s);
   }));
-  CHK(timed(t, "reduce_sgd", [&]() {
-    return xh::launch_slab_reduce(t->pslab, t->pslab_n, t->pslab_stride, t->np,
-                                  t->pgrads, s);
-  }));
-  CHK(allreduce(t, t->pgrads, t->np));
-  CHK(opt_apply(t, XH_POLICY, t->pp, t->pgrads, t->np));
+  CHK(reduce_and_step(t, XH_POLICY, t->pslab, t->pslab_n, t->pslab_stride,
+                      t->np, t->pgrads, t->pp));
   t->need_shift = true;
   return XH_OK;
 }
