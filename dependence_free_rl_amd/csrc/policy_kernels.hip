@@ -53,6 +53,35 @@
   do {                                 \
   } while (0)
 #endif
+#define XH_STAMP4(a, gi, w, lane, slot) XH_STAMP(a, gi, w, lane, slot)
+// Kernel span over all workgroups (trace build): the earliest start and the
+// latest end of any workgroup, on the constant-rate wall clock.
+#if XH_DIAG_TRACE
+#define XH_SPAN(a, which)                                                     \
+  do {                                                                        \
+    if ((a).trace && threadIdx.x == 0) {                                      \
+      unsigned long long *sp = reinterpret_cast<unsigned long long *>(        \
+          (a).trace + kTraceBlocks * kTraceGroups * 8 * kTraceSlots);         \
+      const unsigned long long tnow = (unsigned long long)wall_clock64();     \
+      if ((which) == 0)                                                       \
+        atomicMin(sp, tnow);                                                  \
+      else if ((which) == 3)                                                  \
+        atomicMax(sp + 1, tnow);                                              \
+      if (blockIdx.x < 512) sp[2 + 4 * blockIdx.x + (which)] = tnow;          \
+      if ((which) == 0 && blockIdx.x < 512) {                                 \
+        unsigned hw, xc;                                                      \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));      \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xc));     \
+        sp[2 + 2048 + 2 * blockIdx.x] = hw;                                   \
+        sp[2 + 2048 + 2 * blockIdx.x + 1] = xc;                               \
+      }                                                                       \
+    }                                                                         \
+  } while (0)
+#else
+#define XH_SPAN(a, which) \
+  do {                    \
+  } while (0)
+#endif
 
 namespace xh {
 // 1 in the diagnostic builds (make diag / trace variants), 0 in the product
@@ -975,6 +1004,7 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
 #define XH_V4_L3 1
 #endif
 
+
 // ============================================================ train epoch ==
 // KL = true: kl_ppo_learner's epoch (policy_gradient.h:310-335) -- every row
 // of the state matrix: transitions, then the open trajectories' end rows
@@ -984,8 +1014,13 @@ __global__ __launch_bounds__(256, 1) void eval_argmax_kernel(EvalArgs a) {
 template <class S, bool KL>
 __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  // kernel-level stamps in the last trace group's slots (trace build)
+  XH_SPAN(a, 0);
+  XH_STAMP4(a, kTraceGroups - 1, threadIdx.x >> 6, threadIdx.x & 63, 0);
   stage_params<S>(a.params, lds);
   __syncthreads();
+  XH_STAMP4(a, kTraceGroups - 1, threadIdx.x >> 6, threadIdx.x & 63, 1);
+  XH_SPAN(a, 1);
   constexpr int B = S::B, NIT = S::NIT, NOT = S::NOT;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
             h = lane >> 5;
@@ -1079,6 +1114,9 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
     fetch(blockIdx.x, cur, c_cur, po_cur, A_cur, q_cur, v_cur);
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int gi = (g - (int)blockIdx.x) / (int)gridDim.x;
+    (void)gi;
+    XH_STAMP4(a, gi, w, lane, 0);
     const int gn = g + gridDim.x;
     if (gn < ngroups) fetch(gn, nxt, c_nxt, po_nxt, A_nxt, q_nxt, v_nxt);
     f32x16 pre[S::FJ];
@@ -1119,7 +1157,9 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
         }
       }
     }
+    XH_STAMP4(a, gi, w, lane, 1);
     __syncthreads();
+    XH_STAMP4(a, gi, w, lane, 2);
 
     constexpr bool kOne = S::JW == 1 && S::JH == 1 && !KL;  // KL: spills
     constexpr int kU4 = kOne ? XH_V4_UNROLL : 0;
@@ -1176,6 +1216,7 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
       }
       if (w == 0) accB3 += gz;
     }
+    XH_STAMP4(a, gi, w, lane, 3);
 
     // ---- backward through layer 3 and the layer-2 relu (fwd tiles)
     if (fwd_active) {
@@ -1201,7 +1242,9 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
         }
       }
     }
+    XH_STAMP4(a, gi, w, lane, 4);
     __syncthreads();
+    XH_STAMP4(a, gi, w, lane, 5);
 
     // ---- dW2[o2][i] += sum_r dA2[r][o2] H1[r][i]   (K = 64 rows); the JW
     // independent accumulation chains share the dA2 operand
@@ -1222,6 +1265,7 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 #pragma unroll 4
       for (int s = 0; s < (XH_ABL(a, 1) ? 0 : 32); ++s) dw2_step(s);
     }
+    XH_STAMP4(a, gi, w, lane, 6);
 
     // ---- dH1^T[i][r] = sum_o2 W2[o2][i] dA2[r][o2]; relu'; dW1, db1
     {
@@ -1264,6 +1308,7 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
         }
       }
     }
+    XH_STAMP4(a, gi, w, lane, 7);
     __syncthreads();
     cur = nxt;
     c_cur = c_nxt;
@@ -1272,6 +1317,8 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
     q_cur = q_nxt;
     v_cur = v_nxt;
   }
+  XH_STAMP4(a, kTraceGroups - 1, w, lane, 2);
+  XH_SPAN(a, 2);
   if constexpr (KL) {
     if (w == 0) {
 #pragma unroll
@@ -1304,19 +1351,13 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
   const bool h_active = hrt0 < 2;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    float vb1 = accB1[j], vw3 = accW3[j], vb2 = accB2[j];
+    // sums over the 32 rows of each lane half (DPP: valid in lr >= 16)
+    const float vb1 = half_sum32(accB1[j]), vw3 = half_sum32(accW3[j]),
+                vb2 = half_sum32(accB2[j]);
     float vw1[S::F0];
 #pragma unroll
-    for (int f = 0; f < S::F0; ++f) vw1[f] = accW1[j][f];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      vb1 += __shfl_xor(vb1, o, kWave);
-      vw3 += __shfl_xor(vw3, o, kWave);
-      vb2 += __shfl_xor(vb2, o, kWave);
-#pragma unroll
-      for (int f = 0; f < S::F0; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
-    }
-    if (lr == 0) {
+    for (int f = 0; f < S::F0; ++f) vw1[f] = half_sum32(accW1[j][f]);
+    if (lr == 31) {
       const int i = it_own * 32 + acc_row(j, h);
       const int o2 = o2t * 32 + acc_row(j, h);
       if (h_active) {
@@ -1353,6 +1394,8 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
       dst = L.ob3();
     slab[dst] = v;
   }
+  XH_STAMP4(a, kTraceGroups - 1, w, lane, 3);
+  XH_SPAN(a, 3);
 }
 
 // 8-wave train kernel schedule knobs (A/B variants, make variant; the
@@ -1822,20 +1865,13 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   float *my = scr + w * S::RED;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    float va = sA[j], vb = sB[j], vw3 = accW3[j], vb2 = accB2[j];
+    // sums over the 32 rows of each lane half (DPP: valid in lr >= 16)
+    const float va = half_sum32(sA[j]), vb = half_sum32(sB[j]),
+                vw3 = half_sum32(accW3[j]), vb2 = half_sum32(accB2[j]);
     float vw1[S::D];
 #pragma unroll
-    for (int f = 0; f < S::D; ++f) vw1[f] = accW1[j][f];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      va += __shfl_xor(va, o, kWave);
-      vb += __shfl_xor(vb, o, kWave);
-      vw3 += __shfl_xor(vw3, o, kWave);
-      vb2 += __shfl_xor(vb2, o, kWave);
-#pragma unroll
-      for (int f = 0; f < S::D; ++f) vw1[f] += __shfl_xor(vw1[f], o, kWave);
-    }
-    if (lr == 0) {
+    for (int f = 0; f < S::D; ++f) vw1[f] = half_sum32(accW1[j][f]);
+    if (lr == 31) {
       const int i = q * 32 + acc_row(j, h);
       if constexpr (!kMW1) {
 #pragma unroll
@@ -1948,10 +1984,11 @@ int rollout_grid(int B, int D, int H1, int H2) {
   (void)B; (void)D; (void)H1; (void)H2;
   return 2 * cu_count();
 }
-int policy_train_grid(int B, int D, int H1, int H2) {
+int policy_train_grid(int B, int D, int H1, int H2, int kl) {
 #define X(XB, XD, XH1, XH2)                                     \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {          \
     using S = PShape<XB, XD, XH1, XH2>;                         \
+    (void)kl;                                                   \
     return (S::NIT == 4 && S::NOT == 4) ? cu_count()            \
                                         : S::TOCC * cu_count(); \
   }

@@ -124,6 +124,20 @@ __device__ __forceinline__ float seg_sum(float v) {
   }
   return v;
 }
+// Sum over each lane half (lanes 0-31, 32-63) by DPP only: seg_sum<32>'s
+// four in-row stages, then row_bcast15 adds row 0's (row 2's) sum into row 1
+// (row 3).  Valid in lanes 16-31 and 48-63, with the bits of the xor
+// butterfly (the partner's partial sum is added, float addition commutes).
+__device__ __forceinline__ float half_sum32(float v) {
+  v = dpp_add<0xB1>(v);
+  v = dpp_add<0x4E>(v);
+  v = dpp_add<0x141>(v);
+  v = dpp_add<0x140>(v);
+  // row_bcast15 into rows 1 and 3 only (row_mask 0xA); rows 0 / 2 add 0
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(
+                 0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+}
+
 template <int S>
 __device__ __forceinline__ double seg_sum_d(double v) {
 #pragma unroll

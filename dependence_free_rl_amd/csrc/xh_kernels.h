@@ -273,7 +273,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                hipStream_t s);
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                int grid, hipStream_t s);
-int policy_train_grid(int B, int D, int H1, int H2);
+int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
                               hipStream_t s);
 int rollout_grid(int B, int D, int H1, int H2);

@@ -677,9 +677,12 @@ int do_learn(xh_trainer *t) {
   const size_t trace_n = (size_t)xh::kTraceBlocks * xh::kTraceGroups * 8 *
                          xh::kTraceSlots;
   if (xh::diag_build() && std::getenv("XH_PHASE_TRACE")) {
-    if (!trace_buf && hipMalloc(&trace_buf, trace_n * 8) != hipSuccess)
+    // + the kernel span words: earliest start (init all ones), latest end
+    // and per-workgroup start / end words for 1024 workgroups
+    if (!trace_buf && hipMalloc(&trace_buf, trace_n * 8 + 16 + 4096 * 8) != hipSuccess)
       return fail(XH_ERR_HIP, "trace buffer");
-    if (hipMemsetAsync(trace_buf, 0, trace_n * 8, s) != hipSuccess)
+    if (hipMemsetAsync(trace_buf, 0, trace_n * 8 + 16 + 4096 * 8, s) != hipSuccess ||
+        hipMemsetAsync(trace_buf + trace_n, 0xFF, 8, s) != hipSuccess)
       return fail(XH_ERR_HIP, "trace buffer");
     pa.trace = trace_buf;
   }
@@ -701,8 +704,8 @@ int do_learn(xh_trainer *t) {
                                      s);
     }));
     if (pa.trace) {
-      std::vector<long long> tr(trace_n);
-      if (hipMemcpyAsync(tr.data(), pa.trace, trace_n * 8,
+      std::vector<long long> tr(trace_n + 2 + 4096);
+      if (hipMemcpyAsync(tr.data(), pa.trace, trace_n * 8 + 16 + 4096 * 8,
                          hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess)
         return fail(XH_ERR_HIP, "trace read-back");
@@ -727,6 +730,90 @@ int do_learn(xh_trainer *t) {
                    " dH1 %.0f dW2 %.0f end+bar3 %.0f\n", n,
                    sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n, sum[4] / n,
                    sum[5] / n, sum[6] / n, sum[7] / n, sum[8] / n);
+      {  // kernel-level stamps (4-wave kernel: the last trace group)
+        double k1 = 0, k2 = 0, k3 = 0;
+        long kn = 0;
+        for (int b = 0; b < xh::kTraceBlocks; ++b)
+          for (int w = 0; w < 8; ++w) {
+            const long long *p =
+                &tr[((b * xh::kTraceGroups + xh::kTraceGroups - 1) * 8 + w) *
+                    xh::kTraceSlots];
+            if (!p[0] || !p[3]) continue;
+            k1 += p[1] - p[0];
+            k2 += p[2] - p[1];
+            k3 += p[3] - p[2];
+            ++kn;
+          }
+        if (kn)
+          std::fprintf(stderr, "kernel stamps (%ld waves, cycles): stage %.0f "
+                       "| groups %.0f | epilogue %.0f\n", kn, k1 / kn,
+                       k2 / kn, k3 / kn);
+        int wc = 0;
+        (void)hipDeviceGetAttribute(&wc, hipDeviceAttributeWallClockRate,
+                                    t->ctx->device);
+        if (tr[trace_n + 1] && wc > 0)
+          std::fprintf(stderr, "workgroup span: %.1f us (wall clock %d kHz)\n",
+                       (double)(tr[trace_n + 1] - tr[trace_n]) * 1e3 / wc, wc);
+        if (tr[trace_n + 1] && wc > 0) {  // per-workgroup phase spread
+          // [b][start, staged, loop done, end] on the wall clock
+          std::vector<double> ph[4];
+          for (int b = 0; b < 512; ++b) {
+            const long long *w4 = &tr[trace_n + 2 + 4 * b];
+            if (!w4[0] || !w4[3]) continue;
+            ph[0].push_back((w4[1] - w4[0]) * 1e3 / wc);
+            ph[1].push_back((w4[2] - w4[1]) * 1e3 / wc);
+            ph[2].push_back((w4[3] - w4[2]) * 1e3 / wc);
+            ph[3].push_back((w4[3] - w4[0]) * 1e3 / wc);
+          }
+          auto q = [](std::vector<double> v, double f) {
+            std::sort(v.begin(), v.end());
+            return v.empty() ? 0.0 : v[(size_t)(f * (v.size() - 1))];
+          };
+          const char *nm[4] = {"stage", "groups", "epilogue", "total"};
+          std::fprintf(stderr, "workgroups %zu (us, min/p10/med/p90/max):",
+                       ph[3].size());
+          for (int k = 0; k < 4; ++k)
+            std::fprintf(stderr, " %s %.1f/%.1f/%.1f/%.1f/%.1f", nm[k],
+                         q(ph[k], 0), q(ph[k], .1), q(ph[k], .5), q(ph[k], .9),
+                         q(ph[k], 1));
+          std::fprintf(stderr, "\n");
+          // placement: workgroups per CU (xcc, se, sh, cu from HW_ID /
+          // XCC_ID) and the duration of each CU's pair
+          std::map<long, std::vector<double>> cu;
+          std::map<long, std::vector<int>> cub;
+          for (int b = 0; b < 512; ++b) {
+            const long long *w4 = &tr[trace_n + 2 + 4 * b];
+            if (!w4[0] || !w4[3]) continue;
+            const unsigned hw = (unsigned)tr[trace_n + 2 + 2048 + 2 * b];
+            const unsigned xc = (unsigned)tr[trace_n + 2 + 2048 + 2 * b + 1];
+            const long key = ((long)(xc & 15) << 12) | (((hw >> 13) & 7) << 8) |
+                             (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+            cu[key].push_back((w4[3] - w4[0]) * 1e3 / wc);
+            cub[key].push_back(b);
+          }
+          std::map<size_t, int> per;
+          std::vector<double> pmax, pdiff;
+          for (auto &kv : cu) {
+            per[kv.second.size()]++;
+            if (kv.second.size() == 2) {
+              pmax.push_back(std::max(kv.second[0], kv.second[1]));
+              pdiff.push_back(std::fabs(kv.second[0] - kv.second[1]));
+            }
+          }
+          std::fprintf(stderr, "placement: %zu CUs;", cu.size());
+          for (auto &kv : per) std::fprintf(stderr, " %d CUs with %zu wg;", kv.second, kv.first);
+          std::fprintf(stderr, " pair max dur p10/med/p90 %.1f/%.1f/%.1f, pair |diff| med/p90 %.1f/%.1f\n",
+                       q(pmax, .1), q(pmax, .5), q(pmax, .9), q(pdiff, .5), q(pdiff, .9));
+          int shown = 0;
+          for (auto &kv : cub) {
+            if (shown++ >= 6) break;
+            std::fprintf(stderr, "  cu %05lx: blocks", kv.first);
+            for (size_t i = 0; i < kv.second.size(); ++i)
+              std::fprintf(stderr, " %d(%.1fus)", kv.second[i], cu[kv.first][i]);
+            std::fprintf(stderr, "\n");
+          }
+        }
+      }
       pa.trace = nullptr;  // first epoch only
     }
     // the optimizer step does not read beta: it may precede the KL update
@@ -1226,7 +1313,8 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->vgr[0], T * N * c.value_h1 * 4);
     A(&t->vgr[1], T * N * c.value_h2 * 4);
     t->rgrid = xh::rollout_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
-    t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2);
+    t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2,
+                                       c.algo == XH_KLPPO);
     const int groups = (int)(T * N / (size_t)G);
     if (t->pslab_n > groups) t->pslab_n = groups;
     t->pslab_stride = (t->np + 63) & ~63;
