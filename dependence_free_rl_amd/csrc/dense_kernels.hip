@@ -55,8 +55,9 @@ struct RowsOnes {
 // row r: feature k = bin (k / 2D), c = k % 2D: c < D -> bins[bin][c] / 8,
 // else item[c - D] / 8.  Row r is slot s, env e with s * N + e = list[r]
 // (list == nullptr: slot `slot`, env r).  With `action`, rows r >= term_from
-// are the terminal views E_t of transition q = r - term_from: the state of
-// slot t with bins[action[q]] -= item, taken before the reset (rl.h:336-343).
+// are the terminal views E_t of transition q = r - term_from (or q =
+// term_list[r - term_from]): the state of slot t with bins[action[q]] -=
+// item, taken before the reset (rl.h:336-343).
 struct ObsRows {
   EnvDesc E;
   const int8_t *bins, *items;
@@ -64,6 +65,7 @@ struct ObsRows {
   int N, slot;
   const int32_t *action;
   int term_from;
+  const int *term_list;
   // (slot*N + env, terminal action or -1) of row r: resolved once per row
   struct RowCtx {
     int idx, sub;
@@ -71,7 +73,7 @@ struct ObsRows {
   __device__ RowCtx ctx(int r) const {
     RowCtx c{0, -1};
     if (action && r >= term_from) {
-      c.idx = r - term_from;
+      c.idx = term_list ? term_list[r - term_from] : r - term_from;
       c.sub = action[c.idx];
     } else {
       c.idx = list ? list[r] : slot * N + r;
@@ -277,6 +279,7 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
       la.slot = a.slot;
       la.action = a.action;
       la.term_from = a.term_from;
+      la.term_list = a.term_list;
       e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
     } else {
       RowMajor la{a.act[l - 1], in};
@@ -306,6 +309,7 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
       lb.slot = a.slot;
       lb.action = a.action;
       lb.term_from = a.term_from;
+      lb.term_list = a.term_list;
       lb.ncol = in;
       e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
                splits, s);

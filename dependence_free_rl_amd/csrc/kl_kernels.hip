@@ -1,6 +1,6 @@
 // kl_kernels.hip -- the small device-side steps of kl_ppo_learner
 // (policy_gradient.h:41-85, 310-335) around the KL train epoch:
-//   end_list_kernel   which transitions ended an episode (their terminal end
+//   end_*_kernel      which transitions ended an episode (their terminal end
 //                     rows join the state matrix), and how many trajectories
 //                     are still open (their end rows are the slot-T states);
 //   kl_reduce_kernel  sum of the per-workgroup KL partials (fixed order);
@@ -12,45 +12,125 @@
 
 namespace xh {
 
-// One 1024-thread workgroup.  Entries t*N + e in env-major order (e
-// ascending, then t), so the list -- and every sum over it -- is the same
-// from run to run.
-__global__ __launch_bounds__(1024) void end_list_kernel(EndListArgs a) {
-  __shared__ int scan[1024];
-  __shared__ int open_part[1024];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int chunk = (a.N + nt - 1) / nt;
-  const int e0 = tid * chunk, e1 = min(a.N, e0 + chunk);
-  int cnt = 0, open = 0;
-  for (int e = e0; e < e1; ++e) {
-    for (int t = 0; t < a.T; ++t) cnt += a.done[(size_t)t * a.N + e] != 0;
-    open += a.done[(size_t)(a.T - 1) * a.N + e] == 0;
-  }
-  scan[tid] = cnt;
-  open_part[tid] = open;
+// Entries t*N + e in env-major order (e ascending, then t), so the list --
+// and every sum over it -- is the same from run to run.  Three parallel
+// passes (envs on threads, coalesced done reads): per-block counts and local
+// exclusive scans, one workgroup scanning the block totals, then each env
+// writes its entries.
+constexpr int kELB = 256;  // envs per block
+__device__ __forceinline__ int env_done_count(const EndListArgs &a, int e) {
+  int c = 0;
+  if (e < a.N)
+    for (int t = 0; t < a.T; ++t) c += a.done[(size_t)t * a.N + e] != 0;
+  return c;
+}
+// block-local exclusive scan of v over kELB threads; *total = block sum
+__device__ __forceinline__ int block_excl_scan(int v, int *total) {
+  __shared__ int sc[kELB];
+  const int tid = threadIdx.x;
+  __syncthreads();  // a previous call's reads are done
+  sc[tid] = v;
   __syncthreads();
-  // Hillis-Steele inclusive scan
-  for (int off = 1; off < nt; off <<= 1) {
-    const int v = tid >= off ? scan[tid - off] : 0;
+  for (int off = 1; off < kELB; off <<= 1) {
+    const int u = tid >= off ? sc[tid - off] : 0;
     __syncthreads();
-    scan[tid] += v;
+    sc[tid] += u;
     __syncthreads();
   }
-  int pos = scan[tid] - cnt;
-  for (int e = e0; e < e1; ++e)
+  *total = sc[kELB - 1];
+  return sc[tid] - v;
+}
+__global__ __launch_bounds__(kELB) void end_count_kernel(EndListArgs a,
+                                                         int *blk) {
+  const int e = blockIdx.x * kELB + threadIdx.x;
+  int total;
+  (void)block_excl_scan(env_done_count(a, e), &total);
+  const int open = e < a.N && a.done[(size_t)(a.T - 1) * a.N + e] == 0;
+  int open_total;
+  (void)block_excl_scan(open, &open_total);
+  if (threadIdx.x == 0) {
+    blk[2 * blockIdx.x] = total;
+    blk[2 * blockIdx.x + 1] = open_total;
+  }
+}
+// one workgroup: exclusive scan of the block totals (in place), n_end,
+// n_open, rows_out
+__global__ __launch_bounds__(1024) void end_base_kernel(EndListArgs a, int *blk,
+                                                        int nblk) {
+  __shared__ int sc[1024];
+  __shared__ int carry, ocarry;
+  if (threadIdx.x == 0) carry = ocarry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nblk; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    const int v = b < nblk ? blk[2 * b] : 0;
+    const int o = b < nblk ? blk[2 * b + 1] : 0;
+    sc[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int u = threadIdx.x >= off ? sc[threadIdx.x - off] : 0;
+      __syncthreads();
+      sc[threadIdx.x] += u;
+      __syncthreads();
+    }
+    if (b < nblk) blk[2 * b] = carry + sc[threadIdx.x] - v;
+    const int chunk = sc[1023];
+    __syncthreads();
+    sc[threadIdx.x] = o;  // open counts: ordered tree sum
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+      if (threadIdx.x < off) sc[threadIdx.x] += sc[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      carry += chunk;
+      ocarry += sc[0];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *a.n_end = carry;
+    *a.n_open = ocarry;
+    if (a.rows_out) *a.rows_out = a.rows_base + carry;
+  }
+}
+__global__ __launch_bounds__(kELB) void end_write_kernel(EndListArgs a,
+                                                         const int *blk) {
+  const int e = blockIdx.x * kELB + threadIdx.x;
+  const int c = env_done_count(a, e);
+  int total;
+  int pos = blk[2 * blockIdx.x] + block_excl_scan(c, &total);
+  if (e < a.N)
     for (int t = 0; t < a.T; ++t)
       if (a.done[(size_t)t * a.N + e]) a.end_list[pos++] = t * a.N + e;
-  if (tid == nt - 1) *a.n_end = scan[tid];
-  // open count: ordered tree sum
-  for (int off = nt / 2; off > 0; off >>= 1) {
-    if (tid < off) open_part[tid] += open_part[tid + off];
-    __syncthreads();
-  }
-  if (tid == 0) *a.n_open = open_part[0];
 }
 
-hipError_t launch_end_list(const EndListArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(end_list_kernel, dim3(1), dim3(1024), 0, s, a);
+int end_list_scratch_ints(int N) { return 2 * ((N + kELB - 1) / kELB); }
+
+hipError_t launch_end_list(const EndListArgs &a, int *scratch,
+                               hipStream_t s) {
+  const int nblk = (a.N + kELB - 1) / kELB;
+  hipLaunchKernelGGL(end_count_kernel, dim3(nblk), dim3(kELB), 0, s, a, scratch);
+  hipLaunchKernelGGL(end_base_kernel, dim3(1), dim3(1024), 0, s, a, scratch,
+                     nblk);
+  hipLaunchKernelGGL(end_write_kernel, dim3(nblk), dim3(kELB), 0, s, a, scratch);
+  return hipGetLastError();
+}
+
+__global__ void scatter_list_kernel(const int *list, const int *n,
+                                    const float *src, float *dst) {
+  const int cnt = *n;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt;
+       j += gridDim.x * blockDim.x)
+    dst[list[j]] = src[j];
+}
+
+hipError_t launch_scatter_list(const int *list, const int *n, const float *src,
+                               float *dst, int max_n, hipStream_t s) {
+  int blocks = (max_n + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  hipLaunchKernelGGL(scatter_list_kernel, dim3(blocks), dim3(256), 0, s, list,
+                     n, src, dst);
   return hipGetLastError();
 }
 

@@ -96,14 +96,22 @@ struct PolicyTrainArgs {
 };
 constexpr int kTraceBlocks = 4, kTraceGroups = 32, kTraceSlots = 8;
 
-// End-row bookkeeping for KL-PPO (one 1024-thread workgroup).
+// End-row bookkeeping: the ended transitions (KL-PPO end rows, the value
+// step's terminal views).
 struct EndListArgs {
   const uint8_t *done;   // [T][N]
   int N, T;
   int *end_list;         // [T*N] env-major, t ascending
   int *n_end;            // scalar
   int *n_open;           // scalar: envs whose last step is not terminal
+  int *rows_out;         // optional: *rows_out = rows_base + n_end
+  int rows_base;
 };
+// end_list / n_end / n_open (scratch: end_list_scratch_ints(N) ints).
+int end_list_scratch_ints(int N);
+// dst[list[j]] = src[j] for j < *n (terminal-view values to transition rows)
+hipError_t launch_scatter_list(const int *list, const int *n, const float *src,
+                               float *dst, int max_n, hipStream_t s);
 
 // TD targets and GAE around the value net (the net itself runs on the Dense
 // GEMMs, MlpArgs).
@@ -166,6 +174,7 @@ struct MlpArgs {
   int N, slot;                 // slot used when list == nullptr
   const int32_t *action;       // non-null: rows >= term_from are the terminal
   int term_from;               //   views E_t of transition row - term_from
+  const int *term_list;        //   (or of transition term_list[row - term_from])
   const int *rows;             // device row count (nullptr: max_rows)
   int max_rows;
   int nlayers;
@@ -261,7 +270,7 @@ hipError_t launch_env_init(const EnvDesc &env, Batch b, uint32_t x0,
                            int env_offset, int n_global, hipStream_t s);
 hipError_t launch_env_seed(Batch b, uint32_t x, int env_offset,
                            hipStream_t s);
-hipError_t launch_end_list(const EndListArgs &a, hipStream_t s);
+hipError_t launch_end_list(const EndListArgs &a, int *scratch, hipStream_t s);
 // beta <- adapt(beta, mean KL) (policy_gradient.h:68-80); kl_sum[0] = the
 // (all-reduced) KL sum, rows[0] the (all-reduced) row count.
 hipError_t launch_kl_reduce(const double *kl_part, int nparts, const int *n_end,

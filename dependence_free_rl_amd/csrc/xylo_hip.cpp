@@ -137,6 +137,8 @@ struct xh_trainer {
   // KL-PPO state
   float *qold = nullptr, *beta = nullptr, *kl_log = nullptr;
   int *end_list = nullptr, *n_end = nullptr, *n_open = nullptr;
+  int *vrows = nullptr;  // device: (T+1)N + n_end rows of the first V batch
+  int *end_scratch = nullptr;  // launch_end_list_par's block totals
   double *kl_part = nullptr, *kl_sum = nullptr;
   // optimizers of the policy [0] and value [1] nets (nn.h:589-698)
   struct opt_state {
@@ -613,11 +615,27 @@ int do_learn(xh_trainer *t) {
   const xh_config &c = t->cfg;
   xh::ValueArgs va = t->vargs();
   const int NS = (int)((t->T() + 1) * t->N()), NT = (int)(t->T() * t->N());
+  // the transitions that ended an episode (env-major, t ascending); their
+  // terminal views are the only end rows whose V the targets read
+  xh::EndListArgs ea{t->done, (int)t->N(), (int)t->T(), t->end_list,
+                     t->n_end, t->n_open, t->vrows, NS};
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_end_list(ea, t->end_scratch, s);
+  }));
   // update_value_model (policy_gradient.h:196-218): V over S_0..S_T and the
-  // terminal views E_t in one batch, TD targets and dL/dV = V - target on the
+  // terminal views E_t of the ended transitions in one batch (NS + n_end
+  // rows, a device count), TD targets and dL/dV = V - target on the
   // transition rows (end rows have zero gradient), backward, one step
   xh::MlpArgs vm = value_mlp(t, NS + NT, t->v_state0);
+  vm.rows = t->vrows;
+  vm.term_list = t->end_list;
   CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
+  CHK(timed(t, "value", [&]() {
+    return xh::launch_scatter_list(t->end_list, t->n_end, t->v_state0 + NS,
+                                   t->v_term, NT, s);
+  }));
+  vm.rows = nullptr;
+  vm.term_list = nullptr;
   va.v_state = t->v_state0;
   CHK(timed(t, "value", [&]() {
     return xh::launch_value_targets(va, c.gamma, t->targets, s);
@@ -693,9 +711,7 @@ int do_learn(xh_trainer *t) {
     pa.end_list = t->end_list;
     pa.n_end = t->n_end;
     pa.kl_part = t->kl_part;
-    xh::EndListArgs ea{t->done, (int)t->N(), (int)t->T(), t->end_list,
-                       t->n_end, t->n_open};
-    CHK(timed(t, "kl", [&]() { return xh::launch_end_list(ea, s); }));
+    // end_list / n_end / n_open: built before the value step above
   }
   for (int e = 0; e < c.epochs; ++e) {
     float *g = t->pgrads + (size_t)e * t->np;
@@ -1302,9 +1318,15 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->pp, (size_t)t->np * 4);
     A(&t->vp, (size_t)t->nv * 4);
     A(&t->v_state, (T + 1) * N * 4);
-    // V(S_0..S_T) then V(E_0..E_{T-1}): one forward batch, v_term aliases
+    // V(S_0..S_T) then V(E_t) of the terminal transitions only (end_list
+    // order, n_end rows): one forward batch; v_term receives them by row
     A(&t->v_state0, (2 * T + 1) * N * 4);
-    if (st == XH_OK) t->v_term = t->v_state0 + (T + 1) * N;
+    A(&t->v_term, T * N * 4);
+    A(&t->end_list, T * N * 4);
+    A(&t->n_end, 4);
+    A(&t->n_open, 4);
+    A(&t->vrows, 4);
+    A(&t->end_scratch, (size_t)xh::end_list_scratch_ints((int)N) * 4);
     A(&t->targets, T * N * 4);
     A(&t->adv, T * N * 4);
     A(&t->row_g, T * N * 4);
@@ -1336,9 +1358,6 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
       A(&t->qold, T * N * c.bins * 4);
       A(&t->beta, 4);
       A(&t->kl_log, (size_t)c.epochs * 3 * 4);
-      A(&t->end_list, T * N * 4);
-      A(&t->n_end, 4);
-      A(&t->n_open, 4);
       A(&t->kl_part, (size_t)t->pslab_n * 8);
       A(&t->kl_sum, 2 * 8);
     }

@@ -166,7 +166,8 @@ enum {
   XH_BUF_DONE = 4,     /* uint8 [T][N]                                       */
   XH_BUF_RNG = 5,      /* uint32 [N]   per-env engine state                  */
   XH_BUF_V_STATE = 6,  /* f32   [T+1][N] V(S_t) of the last value eval       */
-  XH_BUF_V_TERM = 7,   /* f32   [T][N]  V(terminal view of step t)           */
+  XH_BUF_V_TERM = 7,   /* f32   [T][N]  V(terminal view of step t); entries  */
+                       /*   of transitions that did not end are unspecified */
   XH_BUF_TARGETS = 8,  /* f32   [T][N]  TD targets                           */
   XH_BUF_ADV = 9,      /* f32   [T][N]  advantages                           */
   XH_BUF_VALUE_GRAD = 10,  /* f32 [value params]  last value gradient        */
