@@ -83,8 +83,10 @@ clean:
 # performance variants of the policy kernels for A/B runs on one box
 # (tools/gpu_variants.sh; loaded through XH_LIB_PATH, never by the product):
 #   make variant V=name VFLAGS="-DXH_DIAG_TRACE=1 ..."
+#   make variant V=name VSRC=dense_kernels VFLAGS="..."  (another source file)
+VSRC ?= policy_kernels
 variant: $(OBJS)
 	@mkdir -p build/$(V)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/policy_kernels.hip -o build/$(V)/policy_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/$(V)/libxylo_hip.so build/$(V)/policy_kernels.o \
-	    $(filter-out $(SRC)/policy_kernels.o,$(OBJS)) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/$(VSRC).hip -o build/$(V)/$(VSRC).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o build/$(V)/libxylo_hip.so build/$(V)/$(VSRC).o \
+	    $(filter-out $(SRC)/$(VSRC).o,$(OBJS)) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

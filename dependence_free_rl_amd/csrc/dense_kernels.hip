@@ -20,7 +20,15 @@
 namespace xh {
 namespace dense {
 
-constexpr int BM = 64, BN = 64, BK = 16, PAD = 4;
+// K slice depth (make variant VSRC=dense_kernels VFLAGS=-DXH_DENSE_BK=..):
+// 32 and 64 measured slower than 16 on the value net (config 5: +0.5%, +2.7%
+// per iteration) -- the obs-gathering loader, not the barriers, sets the pace
+#ifndef XH_DENSE_BK
+#define XH_DENSE_BK 16
+#endif
+constexpr int BM = 64, BN = 64, BK = XH_DENSE_BK, PAD = 4;
+constexpr int NJ = BM * BK / 256;  // slice elements per thread per operand
+static_assert(BK == 16 || BK == 32 || BK == 64, "BK");
 
 // ------------------------------------------------------------- loaders ----
 // Each loader returns element (i, k) of its operand viewed as [I x K]; for A
@@ -171,26 +179,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
   const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
   f32x16 acc = zero16();
 
-  // this thread's 4 (i, kk) positions in a BM x BK (or BN x BK) slice
+  // this thread's NJ (i, kk) positions in a BM x BK (or BN x BK) slice
   auto pos = [&](bool kcontig, int j, int &i, int &kk) {
     if (kcontig) {
       kk = tid & (BK - 1);
-      i = (tid >> 4) + 16 * j;
+      i = tid / BK + (256 / BK) * j;
     } else {
       i = tid & 63;
       kk = (tid >> 6) + 4 * j;
     }
   };
-  float ra[4], rb[4];
+  float ra[NJ], rb[NJ];
   // row contexts of this thread's four A rows (kKContig: i does not depend
   // on the K slice), for loaders that gather rows
   struct NoCtx {};
   using Ctx = std::conditional_t<LA::kRowCtx, typename detail::CtxOf<LA>::type, NoCtx>;
-  Ctx rc[4];
+  Ctx rc[NJ];
   if constexpr (LA::kRowCtx) {
     static_assert(LA::kKContig, "row contexts need fixed rows per thread");
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       int i, kk;
       pos(true, j, i, kk);
       const int m = bm + i;
@@ -199,7 +207,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
   }
   auto fetch = [&](int kb) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       int i, kk;
       pos(LA::kKContig, j, i, kk);
       const int m = bm + i, k = kb + kk;
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       int i, kk;
       pos(LA::kKContig, j, i, kk);
       As[kk][i] = ra[j];
