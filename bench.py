@@ -275,6 +275,12 @@ def main():
     rec = B * D + D + 4 * 4 + 1
     hbm_bytes_per_step = 2 * B * D + rec * (1 + 3 + EPOCHS)
     hbm_gbs = value * hbm_bytes_per_step / 1e9
+    # whole-iteration compute roofline: (1 + 3k) Fp + 5 Fv
+    # algorithmic FLOPs per env-step -- the rollout forward, k epochs of
+    # forward + backward, and the value net's evaluations and step
+    it_flops = ((1 + 3 * EPOCHS) * policy_fwd_flops_per_env_step() +
+                5 * value_fwd_flops_per_row())
+    it_tflops = value * it_flops / 1e12
     if args.config == 3:
         metric = "env-steps/sec (whole node) PPO bin-packing 64-bin"
         workload = "BASELINE config %d: " % (3 if world == 1 else 4)
@@ -313,6 +319,12 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
                      "flops_per_launch": flops_epoch},
+        "iteration_roofline": {"flops_per_env_step": it_flops,
+                               "achieved": round(it_tflops, 2),
+                               "peak": FP32_PEAK_TFLOPS * world,
+                               "unit": "TFLOP/s",
+                               "frac": round(it_tflops /
+                                             (FP32_PEAK_TFLOPS * world), 4)},
         "hbm_roofline": {"bytes_per_env_step": hbm_bytes_per_step,
                          "achieved": round(hbm_gbs, 2),
                          "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
