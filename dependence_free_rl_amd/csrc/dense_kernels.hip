@@ -66,7 +66,8 @@ struct RowsOnes {
 // are the terminal views E_t of transition q = r - term_from (or q =
 // term_list[r - term_from]): the state of slot t with bins[action[q]] -=
 // item, taken before the reset (rl.h:336-343).
-struct ObsRows {
+template <int DC>  // dims, compile time: the feature -> (bin, c) split is
+struct ObsRows {   // a constant division
   EnvDesc E;
   const int8_t *bins, *items;
   const int *list;
@@ -89,30 +90,48 @@ struct ObsRows {
     return c;
   }
   __device__ float feature_at(RowCtx rc, int k) const {
-    const int D = E.D, bin = k / (2 * D), c = k - bin * 2 * D;
-    int v = c < D ? bins[(size_t)rc.idx * E.B * D + bin * D + c]
-                  : items[(size_t)rc.idx * 4 + c - D];
-    if (c < D && bin == rc.sub) v -= items[(size_t)rc.idx * 4 + c];
+    const int bin = k / (2 * DC), c = k - bin * 2 * DC;
+    int v = c < DC ? bins[(size_t)rc.idx * E.B * DC + bin * DC + c]
+                   : items[(size_t)rc.idx * 4 + c - DC];
+    if (c < DC && bin == rc.sub) v -= items[(size_t)rc.idx * 4 + c];
     return (float)v * (1.0f / (float)kCapacity);
   }
   __device__ float feature(int r, int k) const { return feature_at(ctx(r), k); }
 };
-struct ObsA : ObsRows {  // A operand: (m = row, k = feature)
+template <int DC>
+struct ObsA : ObsRows<DC> {  // A operand: (m = row, k = feature)
+  using RowCtx = typename ObsRows<DC>::RowCtx;
   static constexpr bool kKContig = true;
   // a thread's rows are fixed for the whole K loop: the GEMM resolves them
   // once per tile (ctx) instead of once per K slice
   static constexpr bool kRowCtx = true;
-  __device__ float operator()(int r, int k) const { return feature(r, k); }
-  __device__ float at(RowCtx rc, int k) const { return feature_at(rc, k); }
+  __device__ float operator()(int r, int k) const { return this->feature(r, k); }
+  __device__ float at(RowCtx rc, int k) const { return this->feature_at(rc, k); }
 };
-struct ObsOnesB : ObsRows {  // B operand of dW1: (n = feature | 1, k = row)
+template <int DC>
+struct ObsOnesB : ObsRows<DC> {  // B operand of dW1: (n = feature | 1, k = row)
   int ncol;
   static constexpr bool kKContig = false;
   static constexpr bool kRowCtx = false;
   __device__ float operator()(int n, int r) const {
-    return n < ncol ? feature(r, n) : 1.0f;
+    return n < ncol ? this->feature(r, n) : 1.0f;
   }
 };
+// the observation loaders of MlpArgs a, for D = DC
+template <class L>
+__host__ L obs_loader(const MlpArgs &a) {
+  L l;
+  l.E = a.env;
+  l.bins = a.bins;
+  l.items = a.items;
+  l.list = a.list;
+  l.N = a.N;
+  l.slot = a.slot;
+  l.action = a.action;
+  l.term_from = a.term_from;
+  l.term_list = a.term_list;
+  return l;
+}
 
 // ----------------------------------------------------------- epilogues ----
 struct EpBiasAct {  // Y[m][n] = act(c + b[n])
@@ -278,17 +297,16 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
     EpBiasAct ep{a.act[l], out, W + out * in, l + 1 < a.nlayers};
     RowMajor wt{W, in};  // B(n = out unit, k) = W[n][k]
     if (l == 0) {
-      ObsA la;
-      la.E = a.env;
-      la.bins = a.bins;
-      la.items = a.items;
-      la.list = a.list;
-      la.N = a.N;
-      la.slot = a.slot;
-      la.action = a.action;
-      la.term_from = a.term_from;
-      la.term_list = a.term_list;
-      e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
+      auto run = [&](auto la) {
+        return gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1,
+                    s);
+      };
+      if (a.env.D == 1)
+        e = run(obs_loader<ObsA<1>>(a));
+      else if (a.env.D == 2)
+        e = run(obs_loader<ObsA<2>>(a));
+      else
+        e = run(obs_loader<ObsA<3>>(a));
     } else {
       RowMajor la{a.act[l - 1], in};
       e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
@@ -308,19 +326,17 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
     ColMajor dyT{a.grad[l], out};  // A(m = out unit, k = row) = dY[row][m]
     EpSlab es{slab, stride, off, off + out * in, in};
     if (l == 0) {
-      ObsOnesB lb;
-      lb.E = a.env;
-      lb.bins = a.bins;
-      lb.items = a.items;
-      lb.list = a.list;
-      lb.N = a.N;
-      lb.slot = a.slot;
-      lb.action = a.action;
-      lb.term_from = a.term_from;
-      lb.term_list = a.term_list;
-      lb.ncol = in;
-      e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
-               splits, s);
+      auto run = [&](auto lb) {
+        lb.ncol = in;
+        return gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows,
+                    a.rows ? 2 : 0, splits, s);
+      };
+      if (a.env.D == 1)
+        e = run(obs_loader<ObsOnesB<1>>(a));
+      else if (a.env.D == 2)
+        e = run(obs_loader<ObsOnesB<2>>(a));
+      else
+        e = run(obs_loader<ObsOnesB<3>>(a));
     } else {
       RowsOnes lb{a.act[l - 1], in, in};
       e = gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows, a.rows ? 2 : 0,
