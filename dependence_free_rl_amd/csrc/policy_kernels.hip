@@ -433,24 +433,35 @@ __global__ __launch_bounds__(256, 2) void rollout_step_kernel(RolloutArgs a) {
 // relu; layer 2 over it, q, u; + bias; the logit over o2t), so logits are
 // bit-identical.  zl[rt]: the partial logit of row rt*32 + (lane & 31).
 // Measured (tools/gpu_ab_vars.sh): config 3 rollout 2.44 -> 2.19 ms per
-// iteration, config 5 5.09 -> 4.83 ms, at 12 waves per workgroup (3 per SIMD;
-// 4 per SIMD spills at 128 VGPRs, and without the scheduling barriers the
-// operand reads of all four tiles are hoisted: 428 B of spills).
+// iteration at 12 waves per workgroup (3 per SIMD; all four tiles' chains
+// at 4 per SIMD spill at 128 VGPRs, and without the scheduling barriers the
+// operand reads of all four tiles are hoisted: 428 B of spills); config 5
+// 5.09 -> 4.83 ms the same way, 4.63 ms in two-tile passes at 4 per SIMD.
 #ifndef XH_V_RPASS
 #define XH_V_RPASS 1
 #endif
 // waves per workgroup of the wave-per-env rollouts (one workgroup of 12 per
 // CU = 3 waves per SIMD with 168 VGPRs: the r-tile pass keeps four H2 tiles'
 // accumulators; 8 = two workgroups per CU, 4 waves per SIMD, 128 VGPRs)
-#ifndef XH_V_RWAVES
-#define XH_V_RWAVES (XH_V_RPASS ? 12 : 8)
+// H2 tiles per pass of the r-tile pass, per kernel: 4 = all four (layer 1
+// once per r-tile, 12 waves per workgroup = 3 per SIMD), 2 = two passes
+// (layer 1 twice, half the accumulators: 8 waves = 4 per SIMD at 128
+// VGPRs).  Measured: 64 bins 2.19 ms (4) vs 2.28 ms (2) per iteration; 128
+// bins 4.81 ms (4) vs 4.63 ms (2).
+#ifndef XH_V_RTILES64
+#define XH_V_RTILES64 4
 #endif
-constexpr int kRollWaves = XH_V_RWAVES;
+#ifndef XH_V_RTILES128
+#define XH_V_RTILES128 2
+#endif
+constexpr int roll_waves(int tiles) { return XH_V_RPASS && tiles == 4 ? 12 : 8; }
+constexpr int roll_occ(int waves) { return waves == 8 ? 4 : (waves == 12 ? 3 : 2); }
+constexpr int kRollWaves64 = roll_waves(XH_V_RTILES64);
+constexpr int kRollWaves128 = roll_waves(XH_V_RTILES128);
 #ifndef XH_V_RSB
 #define XH_V_RSB 1
 #endif
-constexpr int kRollOcc = kRollWaves == 8 ? 4 : (kRollWaves == 12 ? 3 : 2);
-template <class S>
+template <class S, int OT>
 __device__ __forceinline__ void wave_logits_rpass(const float *lds,
                                                   const RowRaw<S> &cur,
                                                   float (&zl)[2]) {
@@ -460,9 +471,12 @@ __device__ __forceinline__ void wave_logits_rpass(const float *lds,
     float xb[S::S1];
 #pragma unroll
     for (int s = 0; s < S::S1; ++s) xb[s] = row_feature<S>(cur, rt, 2 * s + h);
-    f32x16 pre[4];
+    float z = 0.0f;
+#pragma unroll 1
+    for (int op = 0; op < 4 / OT; ++op) {
+    f32x16 pre[OT];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) pre[o] = zero16();
+    for (int o = 0; o < OT; ++o) pre[o] = zero16();
 #pragma unroll 1
     for (int it = 0; it < 4; ++it) {
       f32x16 t1 = zero16();
@@ -480,30 +494,32 @@ __device__ __forceinline__ void wave_logits_rpass(const float *lds,
         for (int u = 0; u < 4; ++u) t1[4 * q + u] = relu(t1[4 * q + u] + bq[u]);
       }
 #pragma unroll
-      for (int o = 0; o < 4; ++o) {
+      for (int oo = 0; oo < OT; ++oo) {
+        const int o = op * OT + oo;
         const float *wrow = lds + S::L_W2 + (o * 32 + lr) * S::W2S + 4 * h;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 a4 = lds4(wrow + it * 32 + 8 * q);
           const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-          for (int u = 0; u < 4; ++u) pre[o] = mfma32(av[u], t1[4 * q + u], pre[o]);
+          for (int u = 0; u < 4; ++u) pre[oo] = mfma32(av[u], t1[4 * q + u], pre[oo]);
         }
         // keep the scheduler from hoisting every tile's operand reads
         if (XH_V_RSB) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    float z = 0.0f;
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
+    for (int oo = 0; oo < OT; ++oo) {
+      const int o = op * OT + oo;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 bb = lds4(lds + S::L_B2 + o * 32 + 8 * q + 4 * h);
         const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) pre[o][4 * q + u] += bq[u];
+        for (int u = 0; u < 4; ++u) pre[oo][4 * q + u] += bq[u];
       }
-      z += logit_part<S>(lds, pre[o], o);
+      z += logit_part<S>(lds, pre[oo], o);
+    }
     }
     if (rt == 0)
       zl[0] = z;
@@ -522,7 +538,7 @@ __device__ __forceinline__ void wave_logits_rpass(const float *lds,
 // rollout_step_kernel (layer1, layer2, logit_part, the o-ordered logit sum),
 // so logits, probabilities and actions are bit-identical.
 template <class S>
-__global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rollout_wave_kernel(RolloutArgs a) {
   static_assert(S::B == 64 && S::NIT == 4 && S::NOT == 4, "wave rollout: B=64, [128,128]");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
@@ -539,7 +555,7 @@ __global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave_kernel
 #pragma unroll
       for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
     float zl[2] = {0.0f, 0.0f};  // partial logit sums of rows lr / 32 + lr
-    if (XH_V_RPASS) wave_logits_rpass<S>(lds, cur, zl);
+    if (XH_V_RPASS) wave_logits_rpass<S, XH_V_RTILES64>(lds, cur, zl);
 #pragma unroll 1
     for (int o2t = 0; o2t < (XH_V_RPASS ? 0 : 4); ++o2t) {
       const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
@@ -767,7 +783,7 @@ __global__ __launch_bounds__(256, 2) void rollout_step128_kernel(RolloutArgs a) 
 // forward and the sampler and four waves per SIMD to hide the
 // double-precision sampler under the other waves' MFMAs.
 template <class S>
-__global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave128_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(64 * kRollWaves128, roll_occ(kRollWaves128)) void rollout_wave128_kernel(RolloutArgs a) {
   static_assert(S::B == 128 && S::NIT == 4 && S::NOT == 4,
                 "wave rollout: B=128, [128,128]");
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -800,7 +816,7 @@ __global__ __launch_bounds__(64 * kRollWaves, kRollOcc) void rollout_wave128_ker
 #pragma unroll
         for (int s = 0; s < S::S1; ++s) xb[rt][s] = row_feature<S>(cur, rt, 2 * s + h);
       float zl[2] = {0.0f, 0.0f};
-      if (XH_V_RPASS) wave_logits_rpass<S>(lds, cur, zl);
+      if (XH_V_RPASS) wave_logits_rpass<S, XH_V_RTILES128>(lds, cur, zl);
 #pragma unroll 1
       for (int o2t = 0; o2t < (XH_V_RPASS ? 0 : 4); ++o2t) {
         const float *wrow = lds + S::L_W2 + (o2t * 32 + lr) * S::W2S + 4 * h;
@@ -2025,10 +2041,11 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                     (int)rollout_lds<S>());                  \
           wattr = true;                                                      \
         }                                                                    \
-        const int wg = (a.b.N + kRollWaves - 1) / kRollWaves;                \
-        const int wgr = kRollWaves == 8 ? grid : cu_count();                 \
+        constexpr int kRW = kRollWaves128;                                   \
+        const int wg = (a.b.N + kRW - 1) / kRW;                              \
+        const int wgr = kRW == 8 ? grid : cu_count();                        \
         hipLaunchKernelGGL(rollout_wave128_kernel<S>,                        \
-                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRollWaves), \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            rollout_lds<S>(), s, a);                          \
         return hipGetLastError();                                            \
       }                                                                      \
@@ -2042,10 +2059,11 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                     (int)rollout_lds<S>());                  \
           wattr = true;                                                      \
         }                                                                    \
-        const int wg = (ng + kRollWaves - 1) / kRollWaves;                   \
-        const int wgr = kRollWaves == 8 ? grid : cu_count();                 \
+        constexpr int kRW = kRollWaves64;                                    \
+        const int wg = (ng + kRW - 1) / kRW;                                 \
+        const int wgr = kRW == 8 ? grid : cu_count();                        \
         hipLaunchKernelGGL(rollout_wave_kernel<S>,                           \
-                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRollWaves), \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            rollout_lds<S>(), s, a);                          \
         return hipGetLastError();                                            \
       }                                                                      \
