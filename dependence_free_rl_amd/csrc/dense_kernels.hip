@@ -117,6 +117,46 @@ struct ObsOnesB : ObsRows<DC> {  // B operand of dW1: (n = feature | 1, k = row)
     return n < ncol ? this->feature(r, n) : 1.0f;
   }
 };
+// The reduced observation of a row: the B*D bin features, then the D item
+// features once (to_vector repeats the item in every bin's row; layer 0's
+// weights for those copies are pre-summed, reduce_w0_kernel).  Feature k < BD:
+// bin k / DC, dim k % DC; k >= BD: item dim k - BD.
+template <int DC>
+struct ObsRedRows : ObsRows<DC> {
+  using RowCtx = typename ObsRows<DC>::RowCtx;
+  __device__ float red_at(RowCtx rc, int k) const {
+    const int BD = this->E.B * DC;
+    int v;
+    if (k < BD) {
+      const int bin = k / DC, c = k - bin * DC;
+      v = this->bins[(size_t)rc.idx * BD + k];
+      if (bin == rc.sub) v -= this->items[(size_t)rc.idx * 4 + c];
+    } else {
+      v = this->items[(size_t)rc.idx * 4 + (k - BD)];
+    }
+    return (float)v * (1.0f / (float)kCapacity);
+  }
+};
+template <int DC>
+struct ObsRedA : ObsRedRows<DC> {  // A operand: (m = row, k = reduced feature)
+  using RowCtx = typename ObsRows<DC>::RowCtx;
+  static constexpr bool kKContig = true;
+  static constexpr bool kRowCtx = true;
+  __device__ float operator()(int r, int k) const {
+    return this->red_at(this->ctx(r), k);
+  }
+  __device__ float at(RowCtx rc, int k) const { return this->red_at(rc, k); }
+};
+template <int DC>
+struct ObsRedOnesB : ObsRedRows<DC> {  // B of dW1: (n = reduced feature | 1, k = row)
+  int ncol;  // B*D + D
+  static constexpr bool kKContig = false;
+  static constexpr bool kRowCtx = false;
+  __device__ float operator()(int n, int r) const {
+    return n < ncol ? this->red_at(this->ctx(r), n) : 1.0f;
+  }
+};
+
 // the observation loaders of MlpArgs a, for D = DC
 template <class L>
 __host__ L obs_loader(const MlpArgs &a) {
@@ -151,6 +191,24 @@ struct EpReluMask {  // dX[m][n] = H[m][n] > 0 ? c : 0 (relu backward, nn.h:364-
   const float *h;
   __device__ void operator()(int m, int n, int, float c) const {
     dx[(size_t)m * ld + n] = h[(size_t)m * ld + n] > 0.0f ? c : 0.0f;
+  }
+};
+// Layer-0 weight gradient over reduced features n (see ObsRedRows): bin
+// feature (b, c) -> column b*2D + c; item feature c -> its B columns
+// b*2D + D + c (the same row sum, written to each); n == B*D + D -> bias.
+struct EpSlabRed {
+  float *slab;
+  int stride, oW, oB, in, B, D;
+  __device__ void operator()(int m, int n, int split, float c) const {
+    float *s = slab + (size_t)split * stride;
+    const int BD = B * D;
+    if (n < BD) {
+      s[oW + m * in + (n / D) * 2 * D + n % D] = c;
+    } else if (n < BD + D) {
+      for (int b = 0; b < B; ++b) s[oW + m * in + b * 2 * D + D + (n - BD)] = c;
+    } else {
+      s[oB + m] = c;
+    }
   }
 };
 struct EpSlab {  // weight-gradient slab: [A(out x in), b(out)] of one layer
@@ -288,6 +346,26 @@ static int layer_offset(const int *w, int l) {
   return off;
 }
 
+// Layer-0 weights on the reduced observation: out[n][k] for k < B*D is
+// W[n][bin*2D + c], for k = B*D + c the sum over bins (ascending) of the
+// item copies' weights W[n][bin*2D + D + c].
+__global__ void reduce_w0_kernel(const float *W, int out, int B, int D,
+                                 float *red) {
+  const int BD = B * D, K = BD + D, in = 2 * BD;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < out * K;
+       i += gridDim.x * blockDim.x) {
+    const int n = i / K, k = i - n * K;
+    float v;
+    if (k < BD) {
+      v = W[(size_t)n * in + (k / D) * 2 * D + k % D];
+    } else {
+      v = 0.0f;
+      for (int b = 0; b < B; ++b) v += W[(size_t)n * in + b * 2 * D + D + (k - BD)];
+    }
+    red[i] = v;
+  }
+}
+
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
   using namespace dense;
   hipError_t e = hipSuccess;
@@ -296,7 +374,26 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
     const float *W = a.params + layer_offset(a.w, l);
     EpBiasAct ep{a.act[l], out, W + out * in, l + 1 < a.nlayers};
     RowMajor wt{W, in};  // B(n = out unit, k) = W[n][k]
-    if (l == 0) {
+    if (l == 0 && a.w0red) {
+      const int K = a.env.B * a.env.D + a.env.D;
+      int nb = (out * K + 255) / 256;
+      nb = nb > 1024 ? 1024 : nb;
+      hipLaunchKernelGGL(reduce_w0_kernel, dim3(nb), dim3(256), 0, s, W, out,
+                         a.env.B, a.env.D, a.w0red);
+      e = hipGetLastError();
+      if (e != hipSuccess) break;
+      RowMajor wr{a.w0red, K};
+      auto run = [&](auto la) {
+        return gemm(la, wr, ep, a.max_rows, out, K, a.rows, a.rows ? 1 : 0, 1,
+                    s);
+      };
+      if (a.env.D == 1)
+        e = run(obs_loader<ObsRedA<1>>(a));
+      else if (a.env.D == 2)
+        e = run(obs_loader<ObsRedA<2>>(a));
+      else
+        e = run(obs_loader<ObsRedA<3>>(a));
+    } else if (l == 0) {
       auto run = [&](auto la) {
         return gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1,
                     s);
@@ -325,7 +422,21 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
     // [dW | db] = dY^T [X | 1] over the batch rows (nn.h:81-100)
     ColMajor dyT{a.grad[l], out};  // A(m = out unit, k = row) = dY[row][m]
     EpSlab es{slab, stride, off, off + out * in, in};
-    if (l == 0) {
+    if (l == 0 && a.w0red) {
+      const int K = a.env.B * a.env.D + a.env.D;
+      EpSlabRed er{slab, stride, off, off + out * in, in, a.env.B, a.env.D};
+      auto run = [&](auto lb) {
+        lb.ncol = K;
+        return gemm(dyT, lb, er, out, K + 1, a.max_rows, a.rows,
+                    a.rows ? 2 : 0, splits, s);
+      };
+      if (a.env.D == 1)
+        e = run(obs_loader<ObsRedOnesB<1>>(a));
+      else if (a.env.D == 2)
+        e = run(obs_loader<ObsRedOnesB<2>>(a));
+      else
+        e = run(obs_loader<ObsRedOnesB<3>>(a));
+    } else if (l == 0) {
       auto run = [&](auto lb) {
         lb.ncol = in;
         return gemm(dyT, lb, es, out, in + 1, a.max_rows, a.rows,

@@ -177,6 +177,9 @@ struct MlpArgs {
   const int *term_list;        //   (or of transition term_list[row - term_from])
   const int *rows;             // device row count (nullptr: max_rows)
   int max_rows;
+  // optional [w[1]][B*D + D] scratch: layer 0 on the reduced observation
+  // (bins, then the item once -- its B copies' weights pre-summed)
+  float *w0red;
   int nlayers;
   int w[4];
   const float *params;  // flat model::parameters() layout

@@ -130,6 +130,7 @@ struct xh_trainer {
   float *vact[2] = {nullptr, nullptr};  // value layer 1 / 2 outputs
   float *vgr[2] = {nullptr, nullptr};   // their dL/d(pre-activation)
   float *pslab = nullptr, *vslab = nullptr;
+  float *vw0red = nullptr;  // value layer 0 on the reduced observation
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
   float *logits = nullptr, *probs = nullptr;
@@ -606,6 +607,7 @@ xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
   m.grad[0] = t->vgr[0];
   m.grad[1] = t->vgr[1];
   m.grad[2] = t->row_g;
+  m.w0red = t->vw0red;
   return m;
 }
 
@@ -1346,6 +1348,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     t->vslab_stride = (t->nv + 63) & ~63;
     A(&t->pslab, (size_t)t->pslab_n * t->pslab_stride * 4);
     A(&t->vslab, (size_t)t->vslab_n * t->vslab_stride * 4);
+    A(&t->vw0red, (size_t)c.value_h1 * (c.bins * c.dims + c.dims) * 4);
     A(&t->pgrads, (size_t)c.epochs * t->np * 4);
     A(&t->vgrad, (size_t)t->nv * 4);
     A(&t->logits, N * c.bins * 4);
