@@ -1752,10 +1752,18 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
     for (size_t i = 0; i < (size_t)count * BD; ++i)
       if (bins[i] > kBinCapacity)
         return fail(XH_ERR_INVALID, "bin value %d above capacity", bins[i]);
-    for (size_t i = 0; i < (size_t)count * D; ++i)
-      if (items[i] != t->env.item_a[i % D] && items[i] != t->env.item_b[i % D])
-        return fail(XH_ERR_INVALID, "item value %d is not in the item table",
-                    items[i]);
+    // a whole item-table entry (the train kernels carry the item columns of
+    // dW1 as per-entry sums)
+    for (int e = 0; e < count; ++e) {
+      bool is_a = true, is_b = true;
+      for (size_t d = 0; d < D; ++d) {
+        is_a &= items[e * D + d] == t->env.item_a[d];
+        is_b &= items[e * D + d] == t->env.item_b[d];
+      }
+      if (!is_a && !is_b)
+        return fail(XH_ERR_INVALID, "env %d: item is not an item-table entry",
+                    first + e);
+    }
     for (int e = 0; e < count; ++e) {
       std::vector<int8_t> v(BD + D);
       std::memcpy(v.data(), bins + (size_t)e * BD, BD);

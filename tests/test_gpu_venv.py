@@ -201,3 +201,19 @@ def test_trainer_env_state_round_trip(ctx):
     np.testing.assert_array_equal(tr.buffer(BUF_ITEMS)[0, 10:12, :D], ni)
     assert np.isfinite(tr.buffer(BUF_ADV)).all()
     tr.close()
+
+
+def test_trainer_env_state_rejects_mixed_items(ctx):
+    """set_env_state takes whole item-table entries only: at D = 3 the item
+    (4, 2, 1) passes a per-dimension check against (4, 2, 2) / (1, 2, 1) but
+    is neither entry (the train kernels carry dW1's item columns as sums per
+    table entry)."""
+    from dependence_free_rl_amd import Trainer, XhError
+    B, D, N = 8, 3, 8
+    tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=2, widths=(64, 32),
+                 rng_state=3)
+    nb = np.full((1, B, D), 8, np.int8)
+    tr.set_env_state(0, nb, np.array([[1, 2, 1]], np.int8))  # item_b: fine
+    with pytest.raises(XhError, match="item-table entry"):
+        tr.set_env_state(0, nb, np.array([[4, 2, 1]], np.int8))
+    tr.close()
