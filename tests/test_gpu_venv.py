@@ -209,9 +209,9 @@ def test_trainer_env_state_rejects_mixed_items(ctx):
     is neither entry (the train kernels carry dW1's item columns as sums per
     table entry)."""
     from dependence_free_rl_amd import Trainer, XhError
-    B, D, N = 8, 3, 8
-    tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=2, widths=(64, 32),
-                 rng_state=3)
+    B, D, N = 128, 3, 8
+    tr = Trainer(ctx, algo="ac", bins=B, dims=D, num_envs=N, steps=2,
+                 widths=(128, 128), rng_state=3)
     nb = np.full((1, B, D), 8, np.int8)
     tr.set_env_state(0, nb, np.array([[1, 2, 1]], np.int8))  # item_b: fine
     with pytest.raises(XhError, match="item-table entry"):
