@@ -1441,6 +1441,10 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 #ifndef XH_V_L3W
 #define XH_V_L3W 1
 #endif
+//   XH_V_FOLDW: the same for 128-row groups (config 5: 15.90 -> 15.60 ms)
+#ifndef XH_V_FOLDW
+#define XH_V_FOLDW 1
+#endif
 //   XH_V_FOLD: 1 = one env per 64-row group, D = 2: the item features'
 //             layer-1 contribution (the same for every row of the group)
 //             folded into the bias, one of the two layer-1 MFMA steps per
@@ -1466,7 +1470,10 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   static_assert(8 * S::RED <= (S::H1 + S::H2) * S::TS, "scratch fits");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   stage_params<S>(a.params, lds);
-  constexpr bool kFold = XH_V_FOLD && S::HG == 1 && S::G == 1 && S::D == 2;
+  // one env per group (G == 1, B >= 64): the item is the same on every row
+  constexpr bool kFold = XH_V_FOLD && S::G == 1 && (S::HG > 1 ? XH_V_FOLDW : 1);
+  // kFold: layer-1 k-steps over the D bin features only (k = 2s + h < D)
+  constexpr int kS1 = kFold ? (S::D + 1) / 2 : S::S1;
   if (kFold) {
     __syncthreads();
     // b1 + W1[:, item dims] . item / 8 for item_a (e = 0) and item_b (e = 1)
@@ -1546,6 +1553,8 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
     return f < S::F0 ? (float)v / (float)kCapacity : 0.0f;
   };
+  // layer-1 input feature f: under kFold the item features are in the bias
+  auto fold_feat = [&](int f) { return (kFold && f >= S::D) ? 0.0f : feat(f); };
   // kFold: this group's env holds item_b (set per group; wave-uniform)
   bool item_b_grp = false;
   // Layer 1 tile by tile, fused into the layer-2 k-loop, for this wave's
@@ -1563,7 +1572,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     }
     float xb[S::S1];
 #pragma unroll
-    for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
+    for (int s = 0; s < S::S1; ++s) xb[s] = fold_feat(2 * s + h);
     const float *wrow = lds + S::L_W2 + (q * 32 + lr) * S::W2S + 4 * h;
     // layer-1 tile it's MFMA chain (from its biases)
     auto l1 = [&](int it) {
@@ -1580,7 +1589,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
         t[4 * qq + 3] = bb.w;
       }
 #pragma unroll
-      for (int s = 0; s < (kFold ? 1 : S::S1); ++s) {
+      for (int s = 0; s < kS1; ++s) {
         const int k = 2 * s + h;
         const float wa = k < S::F0 ? lds[S::L_W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
         t = mfma32(wa, xb[s], t);
@@ -1616,18 +1625,20 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
   auto write_h1_tile = [&]() {
     float xb[S::S1];
 #pragma unroll
-    for (int s = 0; s < S::S1; ++s) xb[s] = feat(2 * s + h);
+    for (int s = 0; s < S::S1; ++s) xb[s] = fold_feat(2 * s + h);
     f32x16 t1;
+    const float *bsrc = kFold ? lds + S::L_B1F + (item_b_grp ? S::H1 : 0)
+                              : lds + S::L_B1;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
-      const float4 bb = lds4(lds + S::L_B1 + q * 32 + 8 * qq + 4 * h);
+      const float4 bb = lds4(bsrc + q * 32 + 8 * qq + 4 * h);
       t1[4 * qq + 0] = bb.x;
       t1[4 * qq + 1] = bb.y;
       t1[4 * qq + 2] = bb.z;
       t1[4 * qq + 3] = bb.w;
     }
 #pragma unroll
-    for (int s = 0; s < S::S1; ++s) {
+    for (int s = 0; s < kS1; ++s) {
       const int k = 2 * s + h;
       const float wa = k < S::F0 ? lds[S::L_W1 + (q * 32 + lr) * S::F0 + k] : 0.0f;
       t1 = mfma32(wa, xb[s], t1);
@@ -1657,7 +1668,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       A_cur = a.adv[ti];
     }
 
-    if (kFold) {
+    if (kFold && HG == 1) {  // bv_c / iv_c: this group's prefetched row
       bool is_a = true;
 #pragma unroll
       for (int d = 0; d < S::D; ++d) is_a &= iv_c[d] == a.env.item_a[d];
@@ -1667,7 +1678,15 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
     f32x16 pre, pre0 = zero16();  // pre0: 128-row groups only
 #pragma unroll
     for (int hg = 0; hg < HG; ++hg) {
-      if (HG > 1) fetch_row(g, hg, bv_c, iv_c);
+      if (HG > 1) {
+        fetch_row(g, hg, bv_c, iv_c);
+        if (kFold && hg == 0) {  // the group's env (both halves)
+          bool is_a = true;
+#pragma unroll
+          for (int d = 0; d < S::D; ++d) is_a &= iv_c[d] == a.env.item_a[d];
+          item_b_grp = !is_a;
+        }
+      }
       // the last half-group's H1 image is written here; every half-group's
       // pre-activations stay in registers for the backward
       pre = forward(hg == HG - 1);
