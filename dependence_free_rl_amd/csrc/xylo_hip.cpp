@@ -586,6 +586,10 @@ int do_rollout(xh_trainer *t) {
 // The value net (full_layer Fin -> V1 -> V2 -> 1, ppo_training.cc:19-26) as a
 // Dense MLP over `rows` rows: S_0..S_T (row = slot * N + env), then the
 // terminal views E_t of transition row - N(T+1).  `out` receives V.
+// layer 0 of the value net on the reduced observation (dense_kernels.hip)
+#ifndef XH_VALUE_REDUCED
+#define XH_VALUE_REDUCED 1
+#endif
 xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
   xh::MlpArgs m{};
   m.env = t->env;
@@ -607,7 +611,9 @@ xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
   m.grad[0] = t->vgr[0];
   m.grad[1] = t->vgr[1];
   m.grad[2] = t->row_g;
-  m.w0red = t->vw0red;
+  // worth its extra launch from a 256-wide input on (config 2's 64-wide
+  // layer 0 measured 1% slower with it)
+  m.w0red = XH_VALUE_REDUCED && t->vl.Fin >= 256 ? t->vw0red : nullptr;
   return m;
 }
 
