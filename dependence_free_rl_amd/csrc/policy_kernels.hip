@@ -1435,6 +1435,11 @@ __global__ __launch_bounds__(256, S::TOCC) void policy_train_kernel(PolicyTrainA
 #ifndef XH_V_DH1W
 #define XH_V_DH1W 16
 #endif
+//   XH_V_W2U: the dW2 loop's unroll factor in the 128-row kernel: 8 (8 B
+//             of spills) 14.53 ms per epoch against 15.55 ms at 4 (0 B)
+#ifndef XH_V_W2U
+#define XH_V_W2U 8
+#endif
 #ifndef XH_V_L3
 #define XH_V_L3 1
 #endif
@@ -1846,8 +1851,7 @@ __global__ __launch_bounds__(512, 2) void policy_train8_kernel(PolicyTrainArgs a
       // The dH1 tile's relu' / dW1 / db1 VALU work rides along, two
       // accumulator registers per 4-row step, in the MFMAs' shadow
       // (7.63 -> 7.44 ms per epoch against running it after dW2).
-      // 128-row groups unroll by 4: 0 B spill (8 B at 8)
-      constexpr int kUnrollW2 = S::HG > 1 ? 4 : 8;
+      constexpr int kUnrollW2 = S::HG > 1 ? XH_V_W2U : 8;
       const float *pa = DAT + (q * 32 + lr) * S::TS + 32 * h;
       const float *pb0 = H1T + ((2 * rt) * 32 + lr) * S::TS + 32 * h;
       const float *pb1 = H1T + ((2 * rt + 1) * 32 + lr) * S::TS + 32 * h;
