@@ -194,21 +194,21 @@ struct EpReluMask {  // dX[m][n] = H[m][n] > 0 ? c : 0 (relu backward, nn.h:364-
   }
 };
 // Layer-0 weight gradient over reduced features n (see ObsRedRows): bin
-// feature (b, c) -> column b*2D + c; item feature c -> its B columns
-// b*2D + D + c (the same row sum, written to each); n == B*D + D -> bias.
+// feature (b, c) -> column b*2D + c; item feature c -> bin 0's item column
+// D + c only (the other bins' item columns hold the same row sum: the slab
+// reduce reads them from bin 0's, SlabAlias); n == B*D + D -> bias.
 struct EpSlabRed {
   float *slab;
   int stride, oW, oB, in, B, D;
   __device__ void operator()(int m, int n, int split, float c) const {
     float *s = slab + (size_t)split * stride;
     const int BD = B * D;
-    if (n < BD) {
+    if (n < BD)
       s[oW + m * in + (n / D) * 2 * D + n % D] = c;
-    } else if (n < BD + D) {
-      for (int b = 0; b < B; ++b) s[oW + m * in + b * 2 * D + D + (n - BD)] = c;
-    } else {
+    else if (n < BD + D)
+      s[oW + m * in + D + (n - BD)] = c;
+    else
       s[oB + m] = c;
-    }
   }
 };
 struct EpSlab {  // weight-gradient slab: [A(out x in), b(out)] of one layer

@@ -113,8 +113,17 @@ __global__ void adv_normalize_kernel(float *adv, long n, const double *stats,
 // A 256-thread block takes 64 consecutive entries x 4 slab ranges (each
 // wave reads 256-byte rows, enough blocks to cover the chip); the 4 range
 // sums combine in LDS as (s0 + s1) + (s2 + s3).  Returned to wave 0's lanes.
+// slab index whose sums entry i takes (SlabAlias: the bin-0 item column)
+__device__ __forceinline__ int slab_src(int i, const SlabAlias &al) {
+  if (al.B > 0 && i < al.rows * al.in) {
+    const int col = i % al.in, b = col / (2 * al.D);
+    if (b > 0 && col - b * 2 * al.D >= al.D) return i - b * 2 * al.D;
+  }
+  return i;
+}
 __device__ __forceinline__ float slab_sum(const float *slab, int nslab,
-                                          int stride, int n, int i) {
+                                          int stride, int n, int i,
+                                          int src) {
   __shared__ float part[4][64];
   const int p = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int per = (nslab + 3) / 4, k0 = r * per,
@@ -122,7 +131,7 @@ __device__ __forceinline__ float slab_sum(const float *slab, int nslab,
   float s = 0.0f;
   if (i < n) {
 #pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += slab[(size_t)k * stride + i];
+    for (int k = k0; k < k1; ++k) s += slab[(size_t)k * stride + src];
   }
   part[r][p] = s;
   __syncthreads();
@@ -131,9 +140,10 @@ __device__ __forceinline__ float slab_sum(const float *slab, int nslab,
 
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
                                                           int nslab, int stride,
-                                                          int n, float *out) {
+                                                          int n, float *out,
+                                                          SlabAlias al) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float g = slab_sum(slab, nslab, stride, n, i);
+  const float g = slab_sum(slab, nslab, stride, n, i, slab_src(i, al));
   if (threadIdx.x < 64 && i < n) out[i] = g;
 }
 
@@ -185,9 +195,9 @@ __global__ void opt_kernel(float *p, const float *g, float *m, float *v, int n,
 // reduced gradient is still written out for introspection).
 __global__ __launch_bounds__(256) void slab_reduce_opt_kernel(
     const float *slab, int nslab, int stride, int n, float *out, float *p,
-    float *m, float *v, OptStep o) {
+    float *m, float *v, OptStep o, SlabAlias al) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float g = slab_sum(slab, nslab, stride, n, i);
+  const float g = slab_sum(slab, nslab, stride, n, i, slab_src(i, al));
   if (threadIdx.x < 64 && i < n) {
     out[i] = g;
     opt_update(p, m, v, i, g, o);
@@ -235,17 +245,18 @@ hipError_t launch_adv_normalize(float *adv, long n, const double *stats,
 }
 
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
-                              float *out, hipStream_t s) {
+                              float *out, hipStream_t s, SlabAlias al) {
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, s,
-                     slab, nslab, stride, n, out);
+                     slab, nslab, stride, n, out, al);
   return hipGetLastError();
 }
 
 hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
                                   int n, float *out, float *params, float *m,
-                                  float *v, OptStep o, hipStream_t s) {
+                                  float *v, OptStep o, hipStream_t s,
+                                  SlabAlias al) {
   hipLaunchKernelGGL(slab_reduce_opt_kernel, dim3((n + 63) / 64), dim3(256), 0,
-                     s, slab, nslab, stride, n, out, params, m, v, o);
+                     s, slab, nslab, stride, n, out, params, m, v, o, al);
   return hipGetLastError();
 }
 

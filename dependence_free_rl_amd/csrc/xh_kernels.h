@@ -302,8 +302,15 @@ hipError_t launch_adv_stats(const double *part, int nparts, double *stats,
                             hipStream_t s);
 hipError_t launch_adv_normalize(float *adv, long n, const double *stats,
                                 double count, hipStream_t s);
+// Slab entries the value net's reduced layer 0 leaves unwritten: the item
+// columns of bins b > 0 of its first [rows][in] block, whose sums equal bin
+// 0's (EpSlabRed).  B = 0: none.
+struct SlabAlias {
+  int rows, in, B, D;
+};
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
-                              float *out, hipStream_t s);
+                              float *out, hipStream_t s,
+                              SlabAlias al = SlabAlias{0, 0, 0, 0});
 hipError_t launch_sgd(float *params, const float *grad, int n, float lr,
                       float wd, hipStream_t s);
 // momentum_optimizer (kind 1) / adam_optimizer (kind 2), nn.h:630-698: state
@@ -320,6 +327,7 @@ hipError_t launch_opt(float *params, const float *grad, float *m, float *v,
 // fixed-order slab sum (written to out) and the same per-element update.
 hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
                                   int n, float *out, float *params, float *m,
-                                  float *v, OptStep o, hipStream_t s);
+                                  float *v, OptStep o, hipStream_t s,
+                                  SlabAlias al = SlabAlias{0, 0, 0, 0});
 
 }  // namespace xh

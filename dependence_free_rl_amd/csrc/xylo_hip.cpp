@@ -513,18 +513,19 @@ int opt_apply(xh_trainer *t, int which, float *params, const float *grad,
 // Slab reduce -> (all-reduce) -> optimizer step.  One rank: one fused launch
 // (the same sums and updates); more ranks: the all-reduce sits between.
 int reduce_and_step(xh_trainer *t, int which, const float *slab, int nslab,
-                    int stride, int n, float *grad, float *params) {
+                    int stride, int n, float *grad, float *params,
+                    xh::SlabAlias al = xh::SlabAlias{0, 0, 0, 0}) {
   hipStream_t s = t->ctx->stream;
   if (!t->ctx->comm) {
     auto &o = t->opt[which];
     const xh::OptStep st = opt_step(t, which);
     return timed(t, "reduce_sgd", [&]() {
       return xh::launch_slab_reduce_opt(slab, nslab, stride, n, grad, params,
-                                        o.m, o.v, st, s);
+                                        o.m, o.v, st, s, al);
     });
   }
   CHK(timed(t, "reduce_sgd", [&]() {
-    return xh::launch_slab_reduce(slab, nslab, stride, n, grad, s);
+    return xh::launch_slab_reduce(slab, nslab, stride, n, grad, s, al);
   }));
   CHK(allreduce(t, grad, n));
   return opt_apply(t, which, params, grad, n);
@@ -652,8 +653,13 @@ int do_learn(xh_trainer *t) {
   CHK(timed(t, "value", [&]() {
     return xh::mlp_backward(vm, t->vslab, t->vslab_stride, t->vslab_n, s);
   }));
+  // the reduced layer 0 writes bin 0's item columns only (EpSlabRed)
+  const xh::SlabAlias al =
+      vm.w0red ? xh::SlabAlias{t->cfg.value_h1, t->vl.Fin, t->cfg.bins,
+                               t->cfg.dims}
+               : xh::SlabAlias{0, 0, 0, 0};
   CHK(reduce_and_step(t, XH_VALUE, t->vslab, t->vslab_n, t->vslab_stride,
-                      t->nv, t->vgrad, t->vp));
+                      t->nv, t->vgrad, t->vp, al));
   // calculate_advantage (policy_gradient.h:220-281) on post-update values;
   // GAE zeroes V(terminal), the targets above used V(E_t)
   vm.max_rows = NS;
