@@ -12,8 +12,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall \
 OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
-            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/xylo_hip.o
-HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h include/xylo_hip.h
+            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/policy_split_kernels.o \
+            $(SRC)/xylo_hip.o
+HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
 # apps/bin_packing drivers (when the reference tree is present) and our own

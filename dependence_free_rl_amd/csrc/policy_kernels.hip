@@ -2173,6 +2173,8 @@ hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                int grid, hipStream_t s) {
   const int B = a.env.B, D = a.env.D;
+  if (policy_train_split_supported(a, H1, H2) && train_split_enabled())
+    return launch_policy_train_split(a, grid, s);
 #define X(XB, XD, XH1, XH2)                                                  \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
     using S = PShape<XB, XD, XH1, XH2>;                                      \

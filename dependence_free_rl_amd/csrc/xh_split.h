@@ -1,0 +1,125 @@
+// xh_split.h -- f32 GEMMs on the bf16 matrix cores of gfx950 at f32 accuracy.
+//
+// gfx950 runs f32-input MFMA (v_mfma_f32_32x32x2_f32) at 64 FLOP/clk/SIMD,
+// 1/16 of its bf16 rate (v_mfma_f32_32x32x16_bf16: 32x32x16 in 32 cycles).
+// An f32 value splits EXACTLY into three bf16 parts,
+//     x = hi + mid + lo + e,   hi = bf16(x), mid = bf16(x - hi),
+//     lo = bf16(x - hi - mid), |e| <= 2^-24 |x|
+// (each difference is exact by Sterbenz; 8 significand bits per part), and a
+// product of two bf16 values is exact in f32.  A dot product then is
+//     a.b = hi.hi + (hi.mid + mid.hi) + (hi.lo + lo.hi + mid.mid) + d,
+//     |d| <= (2^-23 + 2^-22) sum|a_k b_k|
+// (the dropped mid.lo + lo.mid + lo.lo and the two e terms), i.e. six bf16
+// MFMAs per K=16 slice (192 cycles) in place of eight f32 ones (512 cycles).
+// Against an f32 fmaf chain over K terms, whose worst-case error is
+// (K-1) 2^-24 sum|a_k b_k|, the bound is tighter from K = 8 on (the MFMA
+// adds each instruction's 16 exact products into the f32 accumulator).
+//
+// Operand images in LDS: [rows][128 x bf16] (256-byte rows), one image per
+// part, 16-byte chunks XOR-swizzled so that both the ds_read_b128 row reads
+// (an operand whose k runs along the row) and the ds_read_b64_tr_b16
+// transposed reads (k runs down the rows) of a 32x32x16 operand are
+// bank-conflict-free (cdna_hip_programming.md T10, layout (b)).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace xh {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16s __attribute__((ext_vector_type(16)));
+
+constexpr int kImgRow = 256;  // bytes per image row (128 bf16)
+
+// Byte offset of 16-byte chunk ch (0..15) of row `row`.
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return kImgRow * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// x -> hi + mid + lo (bf16, round to nearest even); the differences are
+// exact in f32.
+__device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  const float r2 = r1 - (float)m;
+  l = (__bf16)r2;
+}
+
+// 32x32x16 bf16 MFMA: lane l (r = l&31, h = l>>5) holds A[r][8h+j] and
+// B[8h+j][r] in element j; C/D as the f32 forms (col = l&31, acc_row).
+__device__ __forceinline__ f32x16s mfma_bf16(bf16x8 a, bf16x8 b, f32x16s c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// The six products of a split pair into acc (small terms first, the
+// hi.hi term last).
+__device__ __forceinline__ f32x16s mfma_split6(const bf16x8 (&a)[3],
+                                               const bf16x8 (&b)[3],
+                                               f32x16s c) {
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[0], b[2], c);
+  c = mfma_bf16(a[2], b[0], c);
+  c = mfma_bf16(a[0], b[1], c);
+  c = mfma_bf16(a[1], b[0], c);
+  c = mfma_bf16(a[0], b[0], c);
+  return c;
+}
+
+// Row read: the 8 bf16 of chunk ch of row `row` of an image.
+__device__ __forceinline__ bf16x8 img_row8(const char *img, int row, int ch) {
+  return *reinterpret_cast<const bf16x8 *>(img + img_off(row, ch));
+}
+
+// Transposed read of a 32x32x16 operand whose k runs down the image rows:
+// lane l gets column c0 + (l&31) of rows k0 + 8h .. k0 + 8h + 7 (h = l>>5),
+// element j = row k0 + 8h + j.  c0 is a multiple of 32.  Two
+// ds_read_b64_tr_b16: per 16-lane group g, lane 4q+p supplies the address of
+// row (k0 + 8h + 4t + q), columns c0 + 16(g&1) + 4p .. +3.  EXEC must be
+// full (every lane of the wave executes this).  l = the lane id (a caller
+// may pass an opaque copy so the address arithmetic is not hoisted).
+__device__ __forceinline__ bf16x8 img_tr8(const char *img, int k0, int c0,
+                                          int l = threadIdx.x & 63) {
+  const int g = l >> 4, li = l & 15;
+  const int q = li >> 2, p = li & 3, h = l >> 5;
+  const int ch = (c0 >> 3) + 2 * (g & 1) + (p >> 1);
+  const int boff = 8 * (p & 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int r0 = k0 + 8 * h + q;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4 *)(img + img_off(r0, ch) + boff));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4 *)(img + img_off(r0 + 4, ch) + boff));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Write a 32x32 f32 tile held in MFMA C layout (lane col = image row
+// `row`, register j = feature c0 + acc_row(j, h)) as its three bf16 parts
+// into three images: registers 4g..4g+3 are 4 consecutive features
+// c0 + 8g + 4h .. +3, one 8-byte store per part.
+__device__ __forceinline__ void img_store_split(char *img_hi, char *img_mid,
+                                                char *img_lo, int row, int c0,
+                                                const f32x16s &v) {
+  const int h = (threadIdx.x & 63) >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bf16x4 ph, pm, pl;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      __bf16 a, b, c;
+      split3(v[4 * g + u], a, b, c);
+      ph[u] = a;
+      pm[u] = b;
+      pl[u] = c;
+    }
+    const int off = img_off(row, (c0 >> 3) + g) + 8 * h;
+    *reinterpret_cast<bf16x4 *>(img_hi + off) = ph;
+    *reinterpret_cast<bf16x4 *>(img_mid + off) = pm;
+    *reinterpret_cast<bf16x4 *>(img_lo + off) = pl;
+  }
+}
+
+}  // namespace xh

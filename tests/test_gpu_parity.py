@@ -10,8 +10,10 @@ values, advantages, gradients, parameters.
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_params_close, golden, noise_mask
-from gpu_helpers import meta, row_index, step_major, trainer_from_golden
+from conftest import (assert_close, assert_grad_close, assert_params_close,
+                      golden, noise_mask)
+from gpu_helpers import (default_lr, meta, row_index, step_major,
+                         trainer_from_golden)
 
 pytestmark = pytest.mark.gpu
 
@@ -90,6 +92,28 @@ def test_rollout_sampling_matches_reference(ctx, name):
         tr.learn()
 
 
+def _magnitude_oracle(g, kv):
+    """The CPU oracle on the golden's initial state, teacher-forced in lockstep
+    with the test: it supplies sum|terms| of every policy-gradient entry
+    (or_model_grad_mag) for the row-summed gradient bound."""
+    from oracle import pyoracle as po
+    B, D, N, T = (int(kv["B"]), int(kv["D"]), int(kv["N"]), int(kv.get("T", 4)))
+    widths = [int(w) for w in kv["widths"].split(",")]
+    algo = kv["algo"]
+    head = po.OR_SOFTMAX_XENT if algo == "ac" else po.OR_SOFTMAX
+    code = {"ppo": po.OR_PPO, "ac": po.OR_AC, "klppo": po.OR_KLPPO}[algo]
+    orc = po.Trainer(code, B, D, N, T, po.perbin_model(2 * D, widths, head),
+                     g["init_policy"], po.full_model(B * 2 * D, [64, 32], 1),
+                     g["init_value"], lr_pi=default_lr(algo, 0),
+                     lr_v=default_lr(algo, 1), wd_pi=float(kv.get("wd_pi", 0.0)),
+                     x0=int(g["x0"][0]))
+    kinds = {"sgd": po.OPT_SGD, "momentum": po.OPT_MOMENTUM, "adam": po.OPT_ADAM}
+    for which, key in ((0, "opt_pi"), (1, "opt_v")):
+        if key in kv:
+            orc.set_optimizer(which, kinds[kv[key]], default_lr(algo, which))
+    return orc
+
+
 @pytest.mark.parametrize("name", ["ppo_b8d2", "ppo_b32d1", "ppo_b64d2", "ac_b8d2",
                                   "ac_b128d3", "klppo_b8d2", "ppo_adam_b8d2",
                                   "ac_mom_b8d2", "ppo_b64d2_n160"])
@@ -97,13 +121,17 @@ def test_learn_matches_reference(ctx, name):
     """Teacher-forced iterations: V, advantages, per-epoch policy gradients,
     value gradient and updated parameters vs the reference learner (sgd, and
     momentum / adam optimizers with their state carried across learn();
-    adam's noise-level entries per conftest.noise_mask)."""
+    adam's noise-level entries per conftest.noise_mask).  Policy gradients
+    are row sums under heavy cancellation: they are held to the stated
+    row-summed bound (conftest.assert_grad_close, both sides fp32), with
+    sum|terms| from the oracle run in lockstep."""
+    from oracle import pyoracle as po
     from dependence_free_rl_amd.trainer import (BUF_ADV, BUF_POLICY_GRADS,
                                                 BUF_V_STATE0, BUF_V_TERM,
                                                 BUF_VALUE_GRAD, POLICY, VALUE)
-    from gpu_helpers import default_lr
     tr, g, kv = trainer_from_golden(ctx, name)
-    N, T = tr.N, tr.T
+    orc = _magnitude_oracle(g, kv)
+    N, T, B = tr.N, tr.T, tr.B
     worst = {}
     adam = {w: kv.get(k) == "adam" for w, k in ((POLICY, "opt_pi"),
                                                (VALUE, "opt_v"))}
@@ -113,6 +141,8 @@ def test_learn_matches_reference(ctx, name):
         tr.set_forced_actions(step_major(g[p + "step_choice"], N, T))
         tr.rollout()
         tr.learn()
+        orc.rollout(forced=np.asarray(g[p + "step_choice"]).reshape(N, T))
+        orc.learn()
         rows = row_index(g, it, T)
         v0, vt, adv = tr.buffer(BUF_V_STATE0), tr.buffer(BUF_V_TERM), tr.buffer(BUF_ADV)
         vrow, arow = [], []
@@ -127,11 +157,14 @@ def test_learn_matches_reference(ctx, name):
             ("values", np.array(vrow), g[p + "values_before"]),
             ("advantages", np.array(arow), g[p + "advantages"]),
             ("value_grad", tr.buffer(BUF_VALUE_GRAD), g[p + "value_grad"]),
-            ("policy_grads", tr.buffer(BUF_POLICY_GRADS), g[p + "policy_grads"]),
         ]
         for what, x, y in checks:
             worst[what] = max(worst.get(what, 0.0),
                               assert_close(x, y, what=p + what))
+        worst["policy_grads"] = max(worst.get("policy_grads", 0.0), assert_grad_close(
+            tr.buffer(BUF_POLICY_GRADS).ravel(), np.asarray(g[p + "policy_grads"]).ravel(),
+            orc.buf(po.BUF_POLICY_GRADS_MAG), n_terms=N * T * B, sides=2,
+            what=p + "policy_grads"))
         for w, what, gk in ((VALUE, "value_params", "value_grad"),
                             (POLICY, "policy_params", "policy_grads")):
             gr = g[p + gk]
