@@ -56,6 +56,20 @@ def select_config(c):
     F0, ALGO, EPOCHS, REF_ITERS = 2 * D, k["algo"], k["epochs"], k["ref_iters"]
     return k
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
+# The config-3/4 train kernel (csrc/policy_split_kernels.hip) runs its GEMMs
+# on the bf16 matrix cores at f32 accuracy: every f32 product as six bf16
+# products of the operands' exact three-part splits, so its MFMA-bound peak
+# in f32-equivalent FLOP/s is the dense bf16 peak (MI355X_MICROARCH.md,
+# ~2.5 PFLOP/s) / 6.
+SPLIT_PEAK_TFLOPS = 2500.0 / 6
+
+
+def train_split_active():
+    """Mirrors policy_train_split_supported() && train_split_enabled() in
+    csrc/policy_split_kernels.hip: the 64-bin 2-D [128,128] shape, PPO or
+    AC, unless XH_TRAIN_KERNEL=f32."""
+    return ((B, D, H1, H2) == (64, 2, 128, 128) and ALGO in ("ppo", "ac") and
+            not os.environ.get("XH_TRAIN_KERNEL", "").startswith("f"))
 HBM_PEAK_GBS = 8000.0
 
 
@@ -147,7 +161,7 @@ def cpu_baseline():
                 n_env, T, iters)}
 
 
-def pmc_traffic(kernel="policy_train"):
+def pmc_traffic(kernel="policy_train", any_shape=False):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     FETCH_SIZE / WRITE_SIZE summary (separate --pmc passes; see
     tools/pmc_summary.py).  Raw counters (FETCH_SIZE is not x2-corrected: the
@@ -164,7 +178,7 @@ def pmc_traffic(kernel="policy_train"):
             summ = json.load(f)
         # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
         s = next((v for k, v in sorted(summ.items())
-                  if k.startswith(kernel) and shape in v.get("kernel", "")
+                  if k.startswith(kernel) and (any_shape or shape in v.get("kernel", ""))
                   and "hbm_bytes" in v), None)
         if s:
             return s["hbm_bytes"], os.path.relpath(path, REPO), s
@@ -261,7 +275,12 @@ def main():
     # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
     avg_ms = ms_pt / max(n_pt, 1)
-    traffic, traffic_src, pmc = pmc_traffic()
+    split = train_split_active()
+    # the split kernel has one shape (config 3 / 4): its summary is keyed by
+    # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
+    traffic, traffic_src, pmc = (pmc_traffic("policy_train_split", any_shape=True)
+                                 if split else pmc_traffic())
+    train_peak = SPLIT_PEAK_TFLOPS if split else FP32_PEAK_TFLOPS
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
@@ -281,6 +300,12 @@ def main():
     it_flops = ((1 + 3 * EPOCHS) * policy_fwd_flops_per_env_step() +
                 5 * value_fwd_flops_per_row())
     it_tflops = value * it_flops / 1e12
+    # roofline time of one env-step: the rollout forward and the value net
+    # at the f32 MFMA peak, the k train epochs at the train kernel's peak;
+    # frac = that time x the measured env-steps/s
+    it_ideal_s = (((policy_fwd_flops_per_env_step() + 5 * value_fwd_flops_per_row()) /
+                   (FP32_PEAK_TFLOPS * 1e12)) +
+                  3 * EPOCHS * policy_fwd_flops_per_env_step() / (train_peak * 1e12))
     if args.config == 3:
         metric = "env-steps/sec (whole node) PPO bin-packing 64-bin"
         workload = "BASELINE config %d: " % (3 if world == 1 else 4)
@@ -309,9 +334,14 @@ def main():
                    "epochs": EPOCHS, "parallelism": "dp%d" % world,
                    "lr_scale_rows": not args.reference_lr},
         "roofline": {"kernel": "policy_train", "bound": "mfma",
-                     "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                     "math": ("f32 operands split exactly into 3 bf16 parts, "
+                              "6 bf16 MFMA products per f32 product, f32 "
+                              "accumulate; peak = dense bf16 peak / 6"
+                              if split else "f32 MFMA (v_mfma_f32_32x32x2_f32)"),
+                     "achieved": round(achieved, 2), "peak": round(train_peak, 1),
                      "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "frac": round(achieved / train_peak, 4),
+                     "frac_of_f32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
                      "traffic_source": traffic_src,
                      "mfma_busy_frac": pmc and pmc.get("mfma_busy_frac"),
@@ -321,10 +351,9 @@ def main():
                      "flops_per_launch": flops_epoch},
         "iteration_roofline": {"flops_per_env_step": it_flops,
                                "achieved": round(it_tflops, 2),
-                               "peak": FP32_PEAK_TFLOPS * world,
                                "unit": "TFLOP/s",
-                               "frac": round(it_tflops /
-                                             (FP32_PEAK_TFLOPS * world), 4)},
+                               "roofline_s_per_env_step": it_ideal_s,
+                               "frac": round(value / world * it_ideal_s, 4)},
         "hbm_roofline": {"bytes_per_env_step": hbm_bytes_per_step,
                          "achieved": round(hbm_gbs, 2),
                          "peak": HBM_PEAK_GBS * world, "unit": "GB/s",

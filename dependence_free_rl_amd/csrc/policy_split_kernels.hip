@@ -33,13 +33,9 @@
 #include "xh_split.h"
 
 // Variant knobs (make variant VSRC=policy_split_kernels VFLAGS=...):
-//   XH_SV_OPQ  1 = LDS addresses from an opaque lane id per phase
 //   XH_SV_ABL  diagnostic timing builds only: bit0 skip the dW1 VALU, bit1
 //              skip dW2, bit2 skip dH1, bit3 skip the layer-2 MFMAs (results
 //              are wrong by design; the product build has 0)
-#ifndef XH_SV_OPQ
-#define XH_SV_OPQ 1
-#endif
 #ifndef XH_SV_ABL
 #define XH_SV_ABL 0
 #endif
@@ -65,7 +61,10 @@ constexpr int F_B1F = F_B3 + 4;            // [2][H1]: b1 + item part, per item
 constexpr int F_Z = F_B1F + 2 * kH1;       // [4][64] partial logits
 constexpr int F_X = F_Z + 4 * 64;          // [2 parity][2 dims][64 rows] bins/8
 constexpr int F_END = F_X + 2 * kD * 64;
-constexpr size_t kLds = L_F + sizeof(float) * F_END;
+// db2 partial sums per lane (dA2 summed over this lane's rows): [wave q][4]
+// [64 lanes] float4, read-modify-written once per group
+constexpr int L_B2A = L_F + sizeof(float) * F_END;
+constexpr size_t kLds = L_B2A + 4 * 4 * 64 * 16;
 static_assert(2 * 128 * kImgRow <= L_W2LO, "W2 images fit the row images");
 static_assert(kLds <= 160 * 1024, "LDS");
 
@@ -129,14 +128,29 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   __syncthreads();
   // W2 fragments of tile q: wl = the A operand of layer 2 (rows o, k = i),
   // wd = the A operand of dH1 (rows i, k = o: transposed reads)
+  // per-lane LDS address bases (xh_split.h): rows rt*32 + lr of the row
+  // images, row q*32 + lr of W2's, the transposed-read bases of column tile
+  // q, stores of rows rt*32 + lr
+  const int rb0_ = row_base(lr, h), rb1_ = row_base(32 + lr, h);
+  const int rbw_ = row_base(q * 32 + lr, h);
+  const int tb0_ = tr_base(lane, 0), tb1_ = tr_base(lane, 1);
+  const int tq0_ = tb0_ ^ (64 * q), tq1_ = tb1_ ^ (64 * q);
+  const int sb0 = st_base(lr, h), sb1 = st_base(32 + lr, h);
+  // Opaque copies per phase: the XORs with the compile-time slice / tile
+  // offsets are then issued where the reads are (one v_xor each) instead of
+  // being hoisted out of the group loop into ~40 extra live registers.
+  auto opq = [](int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
   bf16x8 wl[8][2], wd[8][2];
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const char *img = lds + L_W2 + p * 128 * kImgRow;
-      wl[s][p] = img_row8(img, q * 32 + lr, 2 * s + h);
-      wd[s][p] = img_tr8(img, 16 * s, q * 32);
+      wl[s][p] = ld_row(img, rbw_, s);
+      wd[s][p] = ld_tr(img, tq0_, tq1_, s);
     }
   __syncthreads();  // the W2 images' LDS becomes the row images
 
@@ -145,15 +159,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   const char *w2lo = lds + L_W2LO;
   const int N = a.b.N, T = a.b.T;
   const int ngroups = T * N;
-  // An opaque copy of the lane id per phase: the LDS addresses derived from
-  // it are recomputed where they are used (a few VALU per read) instead of
-  // being hoisted out of the group loop, where the ~100 distinct swizzled
-  // addresses would hold as many registers.
-  auto opaque_lane = [&]() {
-    int v = lane;
-    if (XH_SV_OPQ) asm volatile("" : "+v"(v));
-    return v;
-  };
 
   // dW2 tiles (q, n); dW3 partial sums (lane = row layout); dW1 of feature
   // i = q*32 + lr over this lane half's rows: bin columns w0 / w1 and the dA1
@@ -166,7 +171,10 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     for (int n = 0; n < 4; ++n) accW2[n][j] = 0.0f;
     accW3[j] = 0.0f;
   }
-  float b2s = 0.0f, accB3 = 0.0f, w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
+  float accB3 = 0.0f, w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
+  float4 *b2acc = reinterpret_cast<float4 *>(lds + L_B2A) + q * 4 * 64 + lane;
+#pragma unroll
+  for (int j4 = 0; j4 < 4; ++j4) b2acc[64 * j4] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   int par = 0;  // group parity: the X image double buffer
 
   // Software pipeline over the groups of this workgroup: iteration g runs
@@ -222,7 +230,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         t1[j] = relu(t1[j]);
         maskT |= (tT[j] > 0.0f ? 1u : 0u) << (16 * rt + j);
       }
-      img_store_split(h1i[0], h1i[1], h1i[2], rt * 32 + lr, q * 32, t1);
+      img_store_split_b(h1i[0], h1i[1], h1i[2], rt == 0 ? sb0 : sb1, q * 32, t1);
     }
   };
   if ((int)blockIdx.x < ngroups) {
@@ -251,18 +259,17 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // ---- layer 2 (H2 tile q, both r-tiles) + partial logits
     f32x16s pre[2];
     {
+      const int rb0 = opq(rb0_), rb1 = opq(rb1_), rbw = opq(rbw_);
       pre[0] = lds_acc16(lf + F_B2, q * 32, h);
       pre[1] = pre[0];
-      const int ol = opaque_lane(), olr = ol & 31, oh = ol >> 5;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8 wa[3] = {wl[s][0], wl[s][1],
-                              img_row8(w2lo, q * 32 + olr, 2 * s + oh)};
+        const bf16x8 wa[3] = {wl[s][0], wl[s][1], ld_row(w2lo, rbw, s)};
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
           bf16x8 b[3];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) b[p] = img_row8(h1i[p], rt * 32 + olr, 2 * s + oh);
+          for (int p = 0; p < 3; ++p) b[p] = ld_row(h1i[p], rt == 0 ? rb0 : rb1, s);
           if (!(XH_SV_ABL & 8)) pre[rt] = mfma_split6(wa, b, pre[rt]);
         }
       }
@@ -313,6 +320,15 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       }
       if (q == 0) accB3 += gz;
       const float sw = half_swap(gz);
+      float b2[16];  // db2 partial sums over this lane's rows (LDS between groups)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float4 v = b2acc[64 * j4];
+        b2[4 * j4 + 0] = v.x;
+        b2[4 * j4 + 1] = v.y;
+        b2[4 * j4 + 2] = v.z;
+        b2[4 * j4 + 3] = v.w;
+      }
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         // row rt*32 + lr's gradient: own lane in half rt, else lane ^ 32
@@ -328,30 +344,32 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
             const float v = pre[rt][j];
             accW3[j] += gr * relu(v);
             d[j] = v > 0.0f ? gr * wq[u] : 0.0f;
+            b2[j] += d[j];
           }
         }
-        img_store_split(dai[0], dai[1], dai[2], rt * 32 + lr, q * 32, d);
+        img_store_split_b(dai[0], dai[1], dai[2], rt == 0 ? sb0 : sb1, q * 32, d);
       }
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4)
+        b2acc[64 * j4] = make_float4(b2[4 * j4], b2[4 * j4 + 1], b2[4 * j4 + 2],
+                                     b2[4 * j4 + 3]);
     }
     __syncthreads();
 
-    // ---- dW2 tiles (q, n), K = the 64 rows; db2 from the dA2 fragments
-    // (hi + mid + lo = dA2 to within 2^-24)
+    // ---- dW2 tiles (q, n), K = the 64 rows
     {
-      const int ol = opaque_lane();
+      const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         bf16x8 af[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) af[p] = img_tr8(dai[p], 16 * s, q * 32, ol);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          b2s += ((float)af[0][j] + (float)af[1][j]) + (float)af[2][j];
+        for (int p = 0; p < 3; ++p) af[p] = ld_tr(dai[p], tq0, tq1, s);
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
           bf16x8 bf[3];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) bf[p] = img_tr8(h1i[p], 16 * s, n * 32, ol);
+          for (int p = 0; p < 3; ++p)
+            bf[p] = ld_tr(h1i[p], tb0 ^ (64 * n), tb1 ^ (64 * n), s);
           if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split6(af, bf, accW2[n]);
         }
       }
@@ -364,7 +382,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // r-tile by r-tile, so r-tile 0's VALU overlaps r-tile 1's MFMAs.  Layer
     // 1 of the next group in the same phase.
     {
-      const int ol = opaque_lane(), olr = ol & 31, oh = ol >> 5;
+      const int rb0 = opq(rb0_), rb1 = opq(rb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
       float sg = 0.0f;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
@@ -373,10 +391,10 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          const bf16x8 wa[3] = {wd[s][0], wd[s][1], img_tr8(w2lo, 16 * s, q * 32, ol)};
+          const bf16x8 wa[3] = {wd[s][0], wd[s][1], ld_tr(w2lo, tq0, tq1, s)};
           bf16x8 b[3];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) b[p] = img_row8(dai[p], rt * 32 + olr, 2 * s + oh);
+          for (int p = 0; p < 3; ++p) b[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s);
           if (!(XH_SV_ABL & 4)) dh = mfma_split6(b, wa, dh);
         }
         if (XH_SV_ABL & 1) continue;
@@ -415,8 +433,12 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     for (int j = 0; j < 16; ++j)
       slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] = accW2[n][j];
   {
-    const float v = b2s + __shfl_xor(b2s, 32, kWave);
-    if (h == 0) slab[PL.ob2() + q * 32 + lr] = v;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // db2: sums over the 32 rows of each lane half (valid in lr >= 16)
+      const float s2 = half_sum32(b2acc[64 * (j >> 2)][j & 3]);
+      if (lr == 31) slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2;
+    }
   }
   if (q == 0) {
     float v3 = accB3;

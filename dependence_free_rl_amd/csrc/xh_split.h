@@ -96,6 +96,67 @@ __device__ __forceinline__ bf16x8 img_tr8(const char *img, int k0, int c0,
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// ---- Immediate-offset addressing of the same images.  The XOR swizzle
+// touches only address bits 4-7, so a per-lane base computed once turns every
+// read into at most one v_xor plus the ds_read's immediate offset.
+__device__ __forceinline__ int img_swz(int row) {
+  return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+// Row reads of row R in lane half h: chunk 2s + h of the row is at
+// row_base(R, h) ^ (32 s).
+__device__ __forceinline__ int row_base(int R, int h) {
+  return kImgRow * R + 16 * (h ^ img_swz(R));
+}
+__device__ __forceinline__ bf16x8 ld_row(const char *img, int base, int s) {
+  return *reinterpret_cast<const bf16x8 *>(img + (base ^ (32 * s)));
+}
+// Transposed reads (img_tr8's element order): for lane l and half-fragment t,
+// row 8h + 4t + q of the K-slice and chunk 2(g&1) + (p>>1) of the column
+// tile; the swizzle of rows 16s + .. does not depend on s, and column tile n
+// XORs bits 6-7: operand (k0 = 16 s, c0 = 32 n) = tr_base ^ (64 n), + 4096 s.
+__device__ __forceinline__ int tr_base(int l, int t) {
+  const int g = l >> 4, li = l & 15, q = li >> 2, p = li & 3, h = l >> 5;
+  const int cl = 2 * (g & 1) + (p >> 1);
+  const int B = 4 * q + (cl ^ (2 * h + t));
+  return kImgRow * (8 * h + 4 * t + q) + 16 * B + 8 * (p & 1);
+}
+// b0 / b1: tr_base(l, 0 / 1) ^ (64 n) of the column tile
+__device__ __forceinline__ bf16x8 ld_tr(const char *img, int b0, int b1, int s) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4 *)(img + b0 + 4096 * s));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4 *)(img + b1 + 4096 * s));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// Stores of img_store_split: row R's chunk cg, lane half h's 8 bytes at
+// st_base(R, h) ^ (16 cg).
+__device__ __forceinline__ int st_base(int R, int h) {
+  return kImgRow * R + 16 * img_swz(R) + 8 * h;
+}
+__device__ __forceinline__ void img_store_split_b(char *img_hi, char *img_mid,
+                                                  char *img_lo, int base, int c0,
+                                                  const f32x16s &v) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bf16x4 ph, pm, pl;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      __bf16 a, b, c;
+      split3(v[4 * g + u], a, b, c);
+      ph[u] = a;
+      pm[u] = b;
+      pl[u] = c;
+    }
+    const int off = base ^ (16 * ((c0 >> 3) + g));
+    *reinterpret_cast<bf16x4 *>(img_hi + off) = ph;
+    *reinterpret_cast<bf16x4 *>(img_mid + off) = pm;
+    *reinterpret_cast<bf16x4 *>(img_lo + off) = pl;
+  }
+}
+
 // Write a 32x32 f32 tile held in MFMA C layout (lane col = image row
 // `row`, register j = feature c0 + acc_row(j, h)) as its three bf16 parts
 // into three images: registers 4g..4g+3 are 4 consecutive features

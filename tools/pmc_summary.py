@@ -29,8 +29,9 @@ def per_kernel(path, counter):
 
 
 def short(name):
-    """'void xh::policy_train8_kernel<...>(...)' -> 'policy_train8_kernel'."""
-    m = re.match(r"(?:void )?(?:xh::)?([A-Za-z_0-9]+)", name)
+    """'void xh::policy_train8_kernel<...>(...)' -> 'policy_train8_kernel',
+    'xh::split::policy_train_split_kernel(...)' -> 'policy_train_split_kernel'."""
+    m = re.match(r"(?:void )?(?:[A-Za-z_0-9]+::)*([A-Za-z_0-9]+)", name)
     return m.group(1) if m else name
 
 
