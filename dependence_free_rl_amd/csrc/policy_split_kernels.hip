@@ -39,6 +39,14 @@
 #ifndef XH_SV_ABL
 #define XH_SV_ABL 0
 #endif
+//   XH_SV_PF   1 = explicit one-step operand prefetch in layer 2 and dH1
+#ifndef XH_SV_PF
+#define XH_SV_PF 1
+#endif
+//   XH_SV_PF2  the same in dW2
+#ifndef XH_SV_PF2
+#define XH_SV_PF2 1
+#endif
 
 namespace xh {
 namespace split {
@@ -262,6 +270,29 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       const int rb0 = opq(rb0_), rb1 = opq(rb1_), rbw = opq(rbw_);
       pre[0] = lds_acc16(lf + F_B2, q * 32, h);
       pre[1] = pre[0];
+#if XH_SV_PF
+      // explicit one-step prefetch: step st = (K-slice st/2, r-tile st%2);
+      // its operands are loaded while step st-1's MFMAs run
+      bf16x8 lo_c = ld_row(w2lo, rbw, 0), lo_n = lo_c, b_c[3], b_n[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b_c[p] = ld_row(h1i[p], rb0, 0);
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int s = st >> 1, rt = st & 1;
+        if (st + 1 < 16) {
+          const int s1 = (st + 1) >> 1, r1 = (st + 1) & 1;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b_n[p] = ld_row(h1i[p], r1 ? rb1 : rb0, s1);
+          if (r1 == 0) lo_n = ld_row(w2lo, rbw, s1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 wa[3] = {wl[s][0], wl[s][1], lo_c};
+        if (!(XH_SV_ABL & 8)) pre[rt] = mfma_split6(wa, b_c, pre[rt]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+        if (rt == 1) lo_c = lo_n;
+      }
+#else
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const bf16x8 wa[3] = {wl[s][0], wl[s][1], ld_row(w2lo, rbw, s)};
@@ -273,6 +304,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           if (!(XH_SV_ABL & 8)) pre[rt] = mfma_split6(wa, b, pre[rt]);
         }
       }
+#endif
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         float zp = 0.0f;
@@ -359,6 +391,35 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // ---- dW2 tiles (q, n), K = the 64 rows
     {
       const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
+#if XH_SV_PF2
+      // explicit one-step prefetch over steps st = (K-slice st/4, tile st%4)
+      bf16x8 a_c[3], a_n[3], b_c[3], b_n[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a_c[p] = ld_tr(dai[p], tq0, tq1, 0);
+        b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
+        a_n[p] = a_c[p];
+      }
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int n = st & 3;
+        if (st + 1 < 16) {
+          const int s1 = (st + 1) >> 2, n1 = (st + 1) & 3;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            b_n[p] = ld_tr(h1i[p], tb0 ^ (64 * n1), tb1 ^ (64 * n1), s1);
+            if (n1 == 0) a_n[p] = ld_tr(dai[p], tq0, tq1, s1);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split6(a_c, b_c, accW2[n]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          b_c[p] = b_n[p];
+          if (n == 3) a_c[p] = a_n[p];
+        }
+      }
+#else
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         bf16x8 af[3];
@@ -373,6 +434,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split6(af, bf, accW2[n]);
         }
       }
+#endif
     }
     __syncthreads();  // H1 image consumed: the next group's layer 1 may write
 
@@ -389,6 +451,25 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         f32x16s dh;
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
+#if XH_SV_PF
+        bf16x8 lo_c = ld_tr(w2lo, tq0, tq1, 0), lo_n = lo_c, b_c[3], b_n[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b_c[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, 0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          if (s + 1 < 8) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) b_n[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s + 1);
+            lo_n = ld_tr(w2lo, tq0, tq1, s + 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          const bf16x8 wa[3] = {wd[s][0], wd[s][1], lo_c};
+          if (!(XH_SV_ABL & 4)) dh = mfma_split6(b_c, wa, dh);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+          lo_c = lo_n;
+        }
+#else
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           const bf16x8 wa[3] = {wd[s][0], wd[s][1], ld_tr(w2lo, tq0, tq1, s)};
@@ -397,6 +478,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           for (int p = 0; p < 3; ++p) b[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s);
           if (!(XH_SV_ABL & 4)) dh = mfma_split6(b, wa, dh);
         }
+#endif
         if (XH_SV_ABL & 1) continue;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
