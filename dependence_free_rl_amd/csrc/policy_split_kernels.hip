@@ -47,6 +47,11 @@
 #ifndef XH_SV_PF2
 #define XH_SV_PF2 1
 #endif
+//   XH_SV_RM   1 = dH1's relu mask recomputed (two f32 MFMAs) instead of
+//              carried as a bit mask from layer 1
+#ifndef XH_SV_RM
+#define XH_SV_RM 1
+#endif
 
 namespace xh {
 namespace split {
@@ -229,14 +234,18 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       const float xb = (float)(h == 0 ? xv0 : xv1) / (float)kCapacity;
       if (q == 0) xim[h * 64 + rt * 32 + lr] = xb;
       t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa, xb, t1, 0, 0, 0);
+#if !XH_SV_RM
       f32x16s tT;
 #pragma unroll
       for (int j = 0; j < 16; ++j) tT[j] = b1T;
       tT = __builtin_amdgcn_mfma_f32_32x32x2f32(xb, wa, tT, 0, 0, 0);
+#endif
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         t1[j] = relu(t1[j]);
+#if !XH_SV_RM
         maskT |= (tT[j] > 0.0f ? 1u : 0u) << (16 * rt + j);
+#endif
       }
       img_store_split_b(h1i[0], h1i[1], h1i[2], rt == 0 ? sb0 : sb1, q * 32, t1);
     }
@@ -480,6 +489,20 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         }
 #endif
         if (XH_SV_ABL & 1) continue;
+#if XH_SV_RM
+        // the transposed layer-1 tile again (the same two products as
+        // layer1(): bit-identical), for relu' in this layout
+        f32x16s tT;
+        {
+          const float *b1f = lf + F_B1F + (item_a_cur ? 0 : kH1);
+          const float b1T = b1f[q * 32 + lr];
+          const float wa1 = lf[F_W1 + (q * 32 + lr) * kF0 + h];
+          const float xb = xim[h * 64 + rt * 32 + lr];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) tT[j] = b1T;
+          tT = __builtin_amdgcn_mfma_f32_32x32x2f32(xb, wa1, tT, 0, 0, 0);
+        }
+#endif
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const float4 x0 = lds4(xim + rt * 32 + 8 * g4 + 4 * h);
@@ -489,7 +512,11 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int j = 4 * g4 + u;
+#if XH_SV_RM
+            const float d = tT[j] > 0.0f ? dh[j] : 0.0f;
+#else
             const float d = (mask_cur >> (16 * rt + j)) & 1u ? dh[j] : 0.0f;
+#endif
             sg += d;
             w0 = fmaf(d, xa[u], w0);
             w1 = fmaf(d, xc[u], w1);
