@@ -64,6 +64,15 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 SPLIT_PEAK_TFLOPS = 2500.0 / 6
 
 
+def rollout_split_active():
+    """Mirrors rollout_split() in csrc/policy_kernels.hip: the 64-bin 2-D
+    [128,128] rollout runs layer 2 on the bf16-split GEMM unless
+    XH_ROLLOUT_KERNEL is f32 or 4."""
+    e = os.environ.get("XH_ROLLOUT_KERNEL", "")
+    return ((B, D, H1, H2) == (64, 2, 128, 128) and
+            not (e.startswith("f") or e.strip() == "4"))
+
+
 def train_split_active():
     """Mirrors policy_train_split_supported() && train_split_enabled() in
     csrc/policy_split_kernels.hip: the 64-bin 2-D [128,128] shape, PPO or
@@ -300,11 +309,13 @@ def main():
     it_flops = ((1 + 3 * EPOCHS) * policy_fwd_flops_per_env_step() +
                 5 * value_fwd_flops_per_row())
     it_tflops = value * it_flops / 1e12
-    # roofline time of one env-step: the rollout forward and the value net
-    # at the f32 MFMA peak, the k train epochs at the train kernel's peak;
-    # frac = that time x the measured env-steps/s
-    it_ideal_s = (((policy_fwd_flops_per_env_step() + 5 * value_fwd_flops_per_row()) /
-                   (FP32_PEAK_TFLOPS * 1e12)) +
+    # roofline time of one env-step: the rollout forward at its kernel's
+    # peak (bf16-split at 64 bins), the value net at the f32 MFMA peak, the k
+    # train epochs at the train kernel's peak; frac = that time x the
+    # measured env-steps/s
+    roll_peak = SPLIT_PEAK_TFLOPS if rollout_split_active() else FP32_PEAK_TFLOPS
+    it_ideal_s = (policy_fwd_flops_per_env_step() / (roll_peak * 1e12) +
+                  5 * value_fwd_flops_per_row() / (FP32_PEAK_TFLOPS * 1e12) +
                   3 * EPOCHS * policy_fwd_flops_per_env_step() / (train_peak * 1e12))
     if args.config == 3:
         metric = "env-steps/sec (whole node) PPO bin-packing 64-bin"

@@ -21,6 +21,7 @@
 // H1 and dL/dA2 go through LDS images (row stride +1) once per group.
 #include "xh_device.h"
 #include "xh_kernels.h"
+#include "xh_split.h"
 
 #include <cstdlib>
 
@@ -615,6 +616,137 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
     }
     // lane = row = bin: rows 0..31 in lane half 0, 32..63 in half 1
     const float z = (h ? zl[1] : zl[0]) + lds[S::L_B3];
+    sample_step<S>(a, z, env, 0, lane, cur);
+  }
+}
+
+// ============================== rollout step, wave per env, bf16 split ==
+// The wave-per-env rollout of the 64-bin [128,128] shape with layer 2 on the
+// bf16 matrix cores at f32 accuracy (xh_split.h: six bf16 products of exact
+// three-part splits per f32 product).  Layer 1 (f32 MFMA, the same chain,
+// bias and relu as rollout_wave_kernel) leaves H1 tile `it` of an r-tile in
+// accumulator registers (lane = row, register j = feature acc_row(j, h)); its
+// registers 8s .. 8s+7, split, are directly the B operand of K-slice s of
+// the 32x32x16 MFMA, whose k order is then feature it*32 + 16s + 8(e>>2) +
+// 4h + (e&3) for element e of lane half h.  W2 is staged with the columns
+// of every 16-block permuted to that order (bits 2 and 3 of the column
+// swapped), so each A fragment is one ds_read_b128 of the swizzled image.
+// 2.5x fewer MFMA cycles than rollout_wave_kernel; the logits differ from
+// it in the last places (f32-class: tests/test_gpu_scale.py), the sampler,
+// the env step and everything after are the same code.
+// LDS (bytes): three W2 part images [o][permuted i] (96 KB), then f32 W1
+// [H1][F0], b1, b2, w3, b3.
+struct RollSplitLds {
+  static constexpr int W2 = 0;
+  static constexpr int F = 3 * 128 * kImgRow;
+  static constexpr int W1 = 0, B1 = 512, B2 = B1 + 128, W3 = B2 + 128, B3 = W3 + 128;
+  static constexpr size_t bytes = F + sizeof(float) * (B3 + 4);
+};
+
+template <class S>
+__global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rollout_split_kernel(RolloutArgs a) {
+  static_assert(S::B == 64 && S::D == 2 && S::NIT == 4 && S::NOT == 4,
+                "split rollout: B=64, D=2, [128,128]");
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  char *lds = reinterpret_cast<char *>(ldsf);
+  using L = RollSplitLds;
+  float *lf = reinterpret_cast<float *>(lds + L::F);
+  const PolicyLayout PL{S::F0, S::H1, S::H2};
+  const float *P = a.params;
+  for (int e = threadIdx.x; e < S::H2 * S::H1; e += blockDim.x) {
+    const int o = e >> 7, i = e & 127;
+    // logical column i -> its slot: bits 2 and 3 swapped within the 16-block
+    const int c = (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1);
+    __bf16 x0, x1, x2;
+    split3(P[PL.oW2() + e], x0, x1, x2);
+    const int off = img_off(o, c >> 3) + 2 * (c & 7);
+    *reinterpret_cast<__bf16 *>(lds + L::W2 + off) = x0;
+    *reinterpret_cast<__bf16 *>(lds + L::W2 + 128 * kImgRow + off) = x1;
+    *reinterpret_cast<__bf16 *>(lds + L::W2 + 256 * kImgRow + off) = x2;
+  }
+  for (int i = threadIdx.x; i < S::H1 * S::F0; i += blockDim.x) lf[L::W1 + i] = P[PL.oW1() + i];
+  for (int i = threadIdx.x; i < S::H1; i += blockDim.x) {
+    lf[L::B1 + i] = P[PL.ob1() + i];
+    lf[L::B2 + i] = P[PL.ob2() + i];
+    lf[L::W3 + i] = P[PL.ow3() + i];
+  }
+  if (threadIdx.x == 0) lf[L::B3] = P[PL.ob3()];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int wpb = blockDim.x >> 6;
+  const char *w2i[3] = {lds + L::W2, lds + L::W2 + 128 * kImgRow,
+                        lds + L::W2 + 256 * kImgRow};
+  for (int env = blockIdx.x * wpb + w; env < a.b.N; env += gridDim.x * wpb) {
+    RowRaw<S> cur;
+    fetch_rows<S>(a.b, a.t, env, cur);
+    float zl[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      float xb[S::S1];
+#pragma unroll
+      for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
+      f32x16s pre[4];
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pre[ot][j] = 0.0f;
+#pragma unroll 1
+      for (int it = 0; it < 4; ++it) {
+        // layer-1 tile it: chain, + bias, relu (as rollout_wave_kernel)
+        f32x16 t1 = zero16();
+#pragma unroll
+        for (int s1 = 0; s1 < S::S1; ++s1) {
+          const int k = 2 * s1 + h;
+          t1 = mfma32(lf[L::W1 + (it * 32 + lr) * S::F0 + k], xb[s1], t1);
+        }
+        bf16x8 bfr[2][3];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
+          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float v = relu(t1[4 * q + u] + bq[u]);
+            __bf16 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            const int j = 4 * q + u;
+            bfr[j >> 3][0][j & 7] = p0;
+            bfr[j >> 3][1][j & 7] = p1;
+            bfr[j >> 3][2][j & 7] = p2;
+          }
+        }
+#pragma unroll
+        for (int ot = 0; ot < 4; ++ot) {
+          const int rb = row_base(ot * 32 + lr, h);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) af[p] = ld_row(w2i[p], rb, 2 * it + s);
+            pre[ot] = mfma_split6(af, bfr[s], pre[ot]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      float z = 0.0f;
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        float zp = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
+          const float4 ww = *reinterpret_cast<const float4 *>(lf + L::W3 + ot * 32 + 8 * q + 4 * h);
+          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+          const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) zp += relu(pre[ot][4 * q + u] + bq[u]) * wq[u];
+        }
+        z += zp + __shfl_xor(zp, 32, kWave);
+      }
+      zl[rt] = z;
+    }
+    const float z = (h ? zl[1] : zl[0]) + lf[L::B3];
     sample_step<S>(a, z, env, 0, lane, cur);
   }
 }
@@ -2035,6 +2167,12 @@ static bool rollout4() {
   const char *e = std::getenv("XH_ROLLOUT_KERNEL");
   return e && std::atoi(e) == 4;
 }
+// XH_ROLLOUT_KERNEL=f32 keeps the f32-MFMA wave rollout where the bf16-split
+// one would run (64 bins, [128,128]); read per launch.
+static bool rollout_split() {
+  const char *e = std::getenv("XH_ROLLOUT_KERNEL");
+  return !(e && (e[0] == 'f' || std::atoi(e) == 4));
+}
 
 bool policy_shape_supported(int B, int D, int H1, int H2) {
 #define X(XB, XD, XH1, XH2) \
@@ -2108,6 +2246,24 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         hipLaunchKernelGGL(rollout_wave128_kernel<S>,                        \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            rollout_lds<S>(), s, a);                          \
+        return hipGetLastError();                                            \
+      }                                                                      \
+    }                                                                        \
+    if constexpr (S::B == 64 && S::D == 2 && S::NIT == 4 && S::NOT == 4) {   \
+      if (rollout_split()) {                                                 \
+        static bool sattr = false;                                           \
+        if (!sattr) {                                                        \
+          (void)hipFuncSetAttribute((const void *)rollout_split_kernel<S>,   \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                    (int)RollSplitLds::bytes);               \
+          sattr = true;                                                      \
+        }                                                                    \
+        constexpr int kRW = kRollWaves64;                                    \
+        const int wg = (ng + kRW - 1) / kRW;                                 \
+        const int wgr = kRW == 8 ? grid : cu_count();                        \
+        hipLaunchKernelGGL(rollout_split_kernel<S>,                          \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
+                           RollSplitLds::bytes, s, a);                       \
         return hipGetLastError();                                            \
       }                                                                      \
     }                                                                        \

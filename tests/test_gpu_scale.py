@@ -169,8 +169,9 @@ def test_wave_rollout_matches_4wave(ctx, monkeypatch, algo, N, B, D, T):
             BUF_PROBS, BUF_RNG)
     got = {}
     for kern in ("wave", "4"):
-        if kern == "4":
-            monkeypatch.setenv("XH_ROLLOUT_KERNEL", "4")
+        # the f32-MFMA wave kernel (at 64 bins the default rollout is the
+        # bf16-split one: test_split_rollout_matches_f32)
+        monkeypatch.setenv("XH_ROLLOUT_KERNEL", "4" if kern == "4" else "f32")
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
                      widths=(128, 128), rng_state=99)
         tr.set_params(POLICY, pp)
@@ -355,3 +356,49 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch):
     print("policy-gradient error in u * sum|terms| (max, median):", ratios)
     assert ratios["split"][0] <= 3 * ratios["f32"][0] + 8, ratios
     assert ratios["split"][1] <= 3 * ratios["f32"][1] + 1, ratios
+
+
+def test_split_rollout_matches_f32(ctx, monkeypatch):
+    """Config-3 size: the default 64-bin rollout runs layer 2 on the bf16
+    matrix cores with exactly split f32 operands (rollout_split_kernel).
+    Teacher-forced with the f32 wave kernel's actions, it reproduces the
+    states, items, dones and RNG streams bit for bit and the logits /
+    probabilities / p_old within f32-class rounding; free-running, it picks
+    the same action at all but a rare near-tie."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
+                                                BUF_ITEMS, BUF_LOGITS, BUF_POLD,
+                                                BUF_PROBS, BUF_RNG)
+    B, D, N, T = 64, 2, 32768, 4
+    pp, vp = init_policy(D, 128, 128, seed=21), init_value(B, D, seed=22)
+    bufs = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_LOGITS, BUF_POLD,
+            BUF_PROBS, BUF_RNG)
+
+    def run(kernel, forced=None):
+        if kernel == "f32":
+            monkeypatch.setenv("XH_ROLLOUT_KERNEL", "f32")
+        else:
+            monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
+        tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=N, steps=T,
+                     widths=(128, 128), rng_state=77)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        if forced is not None:
+            tr.set_forced_actions(forced)
+        tr.rollout()
+        out = {b: tr.buffer(b).copy() for b in bufs}
+        tr.close()
+        return out
+
+    ref = run("f32")
+    free = run("split")
+    forced = run("split", forced=ref[BUF_ACTION])
+    for b in (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_RNG):
+        np.testing.assert_array_equal(forced[b], ref[b], err_msg="buffer %d" % b)
+    for b in (BUF_LOGITS, BUF_PROBS, BUF_POLD):
+        np.testing.assert_allclose(forced[b], ref[b], rtol=2e-5, atol=1e-7,
+                                   err_msg="buffer %d" % b)
+    mism = int((free[BUF_ACTION] != ref[BUF_ACTION]).sum())
+    print("free-running split vs f32 rollout: %d of %d actions differ" % (
+        mism, ref[BUF_ACTION].size))
+    assert mism <= 1e-4 * ref[BUF_ACTION].size
