@@ -66,10 +66,10 @@ SPLIT_PEAK_TFLOPS = 2500.0 / 6
 
 def rollout_split_active():
     """Mirrors rollout_split() in csrc/policy_kernels.hip: the 64-bin 2-D
-    [128,128] rollout runs layer 2 on the bf16-split GEMM unless
-    XH_ROLLOUT_KERNEL is f32 or 4."""
+    and 128-bin 3-D [128,128] rollouts run layer 2 on the bf16-split GEMM
+    unless XH_ROLLOUT_KERNEL is f32 or 4."""
     e = os.environ.get("XH_ROLLOUT_KERNEL", "")
-    return ((B, D, H1, H2) == (64, 2, 128, 128) and
+    return ((B, D, H1, H2) in ((64, 2, 128, 128), (128, 3, 128, 128)) and
             not (e.startswith("f") or e.strip() == "4"))
 
 

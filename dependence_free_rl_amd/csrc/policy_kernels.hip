@@ -636,23 +636,23 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
 // the env step and everything after are the same code.
 // LDS (bytes): three W2 part images [o][permuted i] (96 KB), then f32 W1
 // [H1][F0], b1, b2, w3, b3.
+template <class S>
 struct RollSplitLds {
   static constexpr int W2 = 0;
   static constexpr int F = 3 * 128 * kImgRow;
-  static constexpr int W1 = 0, B1 = 512, B2 = B1 + 128, W3 = B2 + 128, B3 = W3 + 128;
+  static constexpr int W1 = 0, B1 = S::H1 * S::F0, B2 = B1 + S::H1, W3 = B2 + S::H2,
+                       B3 = W3 + S::H2;
   static constexpr size_t bytes = F + sizeof(float) * (B3 + 4);
 };
 
+// Stage the split W2 images (columns permuted, see above) and the small
+// parameters of the split rollouts.
 template <class S>
-__global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rollout_split_kernel(RolloutArgs a) {
-  static_assert(S::B == 64 && S::D == 2 && S::NIT == 4 && S::NOT == 4,
-                "split rollout: B=64, D=2, [128,128]");
-  extern __shared__ __attribute__((aligned(16))) float ldsf[];
-  char *lds = reinterpret_cast<char *>(ldsf);
-  using L = RollSplitLds;
+__device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
+                                                    char *lds) {
+  using L = RollSplitLds<S>;
   float *lf = reinterpret_cast<float *>(lds + L::F);
   const PolicyLayout PL{S::F0, S::H1, S::H2};
-  const float *P = a.params;
   for (int e = threadIdx.x; e < S::H2 * S::H1; e += blockDim.x) {
     const int o = e >> 7, i = e & 127;
     // logical column i -> its slot: bits 2 and 3 swapped within the 16-block
@@ -671,82 +671,104 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
     lf[L::W3 + i] = P[PL.ow3() + i];
   }
   if (threadIdx.x == 0) lf[L::B3] = P[PL.ob3()];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
-            h = lane >> 5;
-  const int wpb = blockDim.x >> 6;
+}
+
+// Partial logits (without b3) of the two r-tiles of `cur` (64 rows) by the
+// split layer 2: zl[rt] = the logit sum of row rt*32 + (lane & 31).
+template <class S>
+__device__ __forceinline__ void wave_logits_split(const char *lds,
+                                                  const RowRaw<S> &cur,
+                                                  float (&zl)[2]) {
+  using L = RollSplitLds<S>;
+  const float *lf = reinterpret_cast<const float *>(lds + L::F);
+  const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
   const char *w2i[3] = {lds + L::W2, lds + L::W2 + 128 * kImgRow,
                         lds + L::W2 + 256 * kImgRow};
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    float xb[S::S1];
+#pragma unroll
+    for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
+    f32x16s pre[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) pre[ot][j] = 0.0f;
+#pragma unroll 1
+    for (int it = 0; it < 4; ++it) {
+      // layer-1 tile it: chain, + bias, relu (as rollout_wave_kernel)
+      f32x16 t1 = zero16();
+#pragma unroll
+      for (int s1 = 0; s1 < S::S1; ++s1) {
+        const int k = 2 * s1 + h;
+        const float wa = k < S::F0 ? lf[L::W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+        t1 = mfma32(wa, xb[s1], t1);
+      }
+      bf16x8 bfr[2][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float v = relu(t1[4 * q + u] + bq[u]);
+          __bf16 p0, p1, p2;
+          split3(v, p0, p1, p2);
+          const int j = 4 * q + u;
+          bfr[j >> 3][0][j & 7] = p0;
+          bfr[j >> 3][1][j & 7] = p1;
+          bfr[j >> 3][2][j & 7] = p2;
+        }
+      }
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        const int rb = row_base(ot * 32 + lr, h);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) af[p] = ld_row(w2i[p], rb, 2 * it + s);
+          pre[ot] = mfma_split6(af, bfr[s], pre[ot]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    float z = 0.0f;
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      float zp = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
+        const float4 ww = *reinterpret_cast<const float4 *>(lf + L::W3 + ot * 32 + 8 * q + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+        const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) zp += relu(pre[ot][4 * q + u] + bq[u]) * wq[u];
+      }
+      z += zp + __shfl_xor(zp, 32, kWave);
+    }
+    zl[rt] = z;
+  }
+}
+
+template <class S>
+__global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rollout_split_kernel(RolloutArgs a) {
+  static_assert(S::B == 64 && S::NIT == 4 && S::NOT == 4,
+                "split rollout: B=64, [128,128]");
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  char *lds = reinterpret_cast<char *>(ldsf);
+  stage_split_rollout<S>(a.params, lds);
+  __syncthreads();
+  const float b3 = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F)[RollSplitLds<S>::B3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int wpb = blockDim.x >> 6;
   for (int env = blockIdx.x * wpb + w; env < a.b.N; env += gridDim.x * wpb) {
     RowRaw<S> cur;
     fetch_rows<S>(a.b, a.t, env, cur);
-    float zl[2] = {0.0f, 0.0f};
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      float xb[S::S1];
-#pragma unroll
-      for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
-      f32x16s pre[4];
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) pre[ot][j] = 0.0f;
-#pragma unroll 1
-      for (int it = 0; it < 4; ++it) {
-        // layer-1 tile it: chain, + bias, relu (as rollout_wave_kernel)
-        f32x16 t1 = zero16();
-#pragma unroll
-        for (int s1 = 0; s1 < S::S1; ++s1) {
-          const int k = 2 * s1 + h;
-          t1 = mfma32(lf[L::W1 + (it * 32 + lr) * S::F0 + k], xb[s1], t1);
-        }
-        bf16x8 bfr[2][3];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
-          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float v = relu(t1[4 * q + u] + bq[u]);
-            __bf16 p0, p1, p2;
-            split3(v, p0, p1, p2);
-            const int j = 4 * q + u;
-            bfr[j >> 3][0][j & 7] = p0;
-            bfr[j >> 3][1][j & 7] = p1;
-            bfr[j >> 3][2][j & 7] = p2;
-          }
-        }
-#pragma unroll
-        for (int ot = 0; ot < 4; ++ot) {
-          const int rb = row_base(ot * 32 + lr, h);
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            bf16x8 af[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) af[p] = ld_row(w2i[p], rb, 2 * it + s);
-            pre[ot] = mfma_split6(af, bfr[s], pre[ot]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      float z = 0.0f;
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        float zp = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
-          const float4 ww = *reinterpret_cast<const float4 *>(lf + L::W3 + ot * 32 + 8 * q + 4 * h);
-          const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
-          const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) zp += relu(pre[ot][4 * q + u] + bq[u]) * wq[u];
-        }
-        z += zp + __shfl_xor(zp, 32, kWave);
-      }
-      zl[rt] = z;
-    }
-    const float z = (h ? zl[1] : zl[0]) + lf[L::B3];
+    float zl[2];
+    wave_logits_split<S>(lds, cur, zl);
+    const float z = (h ? zl[1] : zl[0]) + b3;
     sample_step<S>(a, z, env, 0, lane, cur);
   }
 }
@@ -1015,6 +1037,54 @@ __global__ __launch_bounds__(64 * kRollWaves128, roll_occ(kRollWaves128)) void r
     sample_step128<S>(a, env, z);
   }
 }
+
+// The 128-bin wave rollout (config 5) with the split layer 2: each env's two
+// 64-row half-groups through wave_logits_split, then sample_step128 as in
+// rollout_wave128_kernel.  3 waves per SIMD (168 VGPRs).
+constexpr int kRollWavesS128 = 12;
+template <class S>
+__global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kernel(RolloutArgs a) {
+  static_assert(S::B == 128 && S::NIT == 4 && S::NOT == 4,
+                "split rollout: B=128, [128,128]");
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  char *lds = reinterpret_cast<char *>(ldsf);
+  stage_split_rollout<S>(a.params, lds);
+  __syncthreads();
+  const float b3 = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F)[RollSplitLds<S>::B3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
+            h = lane >> 5;
+  const int wpb = blockDim.x >> 6;
+  const int N = a.b.N, t = a.t;
+  for (int env = blockIdx.x * wpb + w; env < N; env += gridDim.x * wpb) {
+    float z[2];
+#pragma unroll 1
+    for (int hg = 0; hg < 2; ++hg) {
+      RowRaw<S> cur;
+      const size_t e = (size_t)t * N + env;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int bin = hg * 64 + rt * 32 + lr;
+        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
+        const int8_t *ip = a.b.items + e * 4;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          cur.bv[rt][d] = bp[d];
+          cur.iv[rt][d] = ip[d];
+        }
+      }
+      float zl[2];
+      wave_logits_split<S>(lds, cur, zl);
+      // lane = row of the half-group = bin hg*64 + lane
+      const float zh = (h ? zl[1] : zl[0]) + b3;
+      if (hg == 0)
+        z[0] = zh;
+      else
+        z[1] = zh;
+    }
+    sample_step128<S>(a, env, z);
+  }
+}
+
 
 // ======================================================= argmax evaluation ==
 // Whole episodes inside one launch: the G envs of a group keep their state in
@@ -2167,8 +2237,8 @@ static bool rollout4() {
   const char *e = std::getenv("XH_ROLLOUT_KERNEL");
   return e && std::atoi(e) == 4;
 }
-// XH_ROLLOUT_KERNEL=f32 keeps the f32-MFMA wave rollout where the bf16-split
-// one would run (64 bins, [128,128]); read per launch.
+// XH_ROLLOUT_KERNEL=f32 keeps the f32-MFMA wave rollouts where the
+// bf16-split ones would run (64 / 128 bins, [128,128]); read per launch.
 static bool rollout_split() {
   const char *e = std::getenv("XH_ROLLOUT_KERNEL");
   return !(e && (e[0] == 'f' || std::atoi(e) == 4));
@@ -2232,6 +2302,24 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
     }                                                                        \
     const int ng = a.b.N / S::G;                                             \
     if constexpr (S::B == 128 && S::NIT == 4 && S::NOT == 4) {               \
+      if (rollout_split()) {                                                 \
+        static bool sattr = false;                                           \
+        if (!sattr) {                                                        \
+          (void)hipFuncSetAttribute((const void *)rollout_split128_kernel<S>,\
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,\
+                                    (int)RollSplitLds<S>::bytes);            \
+          sattr = true;                                                      \
+        }                                                                    \
+        constexpr int kRW = kRollWavesS128;                                  \
+        const int wg = (a.b.N + kRW - 1) / kRW;                              \
+        const int wgr = cu_count();                                          \
+        hipLaunchKernelGGL(rollout_split128_kernel<S>,                       \
+                           dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
+                           RollSplitLds<S>::bytes, s, a);                    \
+        return hipGetLastError();                                            \
+      }                                                                      \
+    }                                                                        \
+    if constexpr (S::B == 128 && S::NIT == 4 && S::NOT == 4) {               \
       if (!rollout4()) {                                                     \
         static bool wattr = false;                                           \
         if (!wattr) {                                                        \
@@ -2249,13 +2337,13 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         return hipGetLastError();                                            \
       }                                                                      \
     }                                                                        \
-    if constexpr (S::B == 64 && S::D == 2 && S::NIT == 4 && S::NOT == 4) {   \
+    if constexpr (S::B == 64 && S::NIT == 4 && S::NOT == 4) {                \
       if (rollout_split()) {                                                 \
         static bool sattr = false;                                           \
         if (!sattr) {                                                        \
           (void)hipFuncSetAttribute((const void *)rollout_split_kernel<S>,   \
                                     hipFuncAttributeMaxDynamicSharedMemorySize,\
-                                    (int)RollSplitLds::bytes);               \
+                                    (int)RollSplitLds<S>::bytes);               \
           sattr = true;                                                      \
         }                                                                    \
         constexpr int kRW = kRollWaves64;                                    \
@@ -2263,7 +2351,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         const int wgr = kRW == 8 ? grid : cu_count();                        \
         hipLaunchKernelGGL(rollout_split_kernel<S>,                          \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
-                           RollSplitLds::bytes, s, a);                       \
+                           RollSplitLds<S>::bytes, s, a);                       \
         return hipGetLastError();                                            \
       }                                                                      \
     }                                                                        \
