@@ -75,9 +75,10 @@ def rollout_split_active():
 
 def train_split_active():
     """Mirrors policy_train_split_supported() && train_split_enabled() in
-    csrc/policy_split_kernels.hip: the 64-bin 2-D [128,128] shape, PPO or
-    AC, unless XH_TRAIN_KERNEL=f32."""
-    return ((B, D, H1, H2) == (64, 2, 128, 128) and ALGO in ("ppo", "ac") and
+    csrc/policy_split_kernels.hip: the 64-bin 2-D and 128-bin 3-D [128,128]
+    shapes, PPO or AC, unless XH_TRAIN_KERNEL=f32."""
+    return ((B, D, H1, H2) in ((64, 2, 128, 128), (128, 3, 128, 128)) and
+            ALGO in ("ppo", "ac") and
             not os.environ.get("XH_TRAIN_KERNEL", "").startswith("f"))
 HBM_PEAK_GBS = 8000.0
 
@@ -285,9 +286,10 @@ def main():
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
     avg_ms = ms_pt / max(n_pt, 1)
     split = train_split_active()
-    # the split kernel has one shape (config 3 / 4): its summary is keyed by
+    # the split kernels have one shape each: their summaries are keyed by
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
-    traffic, traffic_src, pmc = (pmc_traffic("policy_train_split", any_shape=True)
+    split_name = ("policy_train_split128" if B == 128 else "policy_train_split_kernel")
+    traffic, traffic_src, pmc = (pmc_traffic(split_name, any_shape=True)
                                  if split else pmc_traffic())
     train_peak = SPLIT_PEAK_TFLOPS if split else FP32_PEAK_TFLOPS
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,

@@ -316,9 +316,12 @@ def test_c3_reference_lr_on_row_sums_diverges(ctx):
     assert first is not None
 
 
-def test_split_train_kernel_accuracy(ctx, monkeypatch):
-    """The config-3 train kernel runs its three 128x128 GEMMs as six bf16
-    MFMAs per K-slice on exactly split f32 operands (csrc/xh_split.h).  Its
+@pytest.mark.parametrize("algo,B,D,N,T", [("ppo", 64, 2, 160, 4),
+                                         ("ac", 128, 3, 24, 8)])
+def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T):
+    """The config-3 and config-5 train kernels run their three 128x128 GEMMs
+    as six bf16 MFMAs per K-slice on exactly split f32 operands
+    (csrc/xh_split.h).  Its
     policy gradients stay within the stated row-summed bound and within a
     small factor of the f32-MFMA kernel's distance to the oracle's
     double-precision sums on the same batch (640 row groups, several per
@@ -328,10 +331,10 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch):
     from oracle import pyoracle as po
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import BUF_POLICY_GRADS
-    B, D, widths, N, T, x0 = 64, 2, (128, 128), 160, 4, 24681357
+    widths, x0 = (128, 128), 24681357
     pp = init_policy(D, *widths, seed=11)
     vp = init_value(B, D, seed=12)
-    orc = _oracle_trainer(B, D, N, T, widths, pp, vp, x0, "ppo")
+    orc = _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo)
     orc.rollout()
     orc.learn()
     ref = orc.buf(po.BUF_POLICY_GRADS)
@@ -342,7 +345,7 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch):
             monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
         else:
             monkeypatch.delenv("XH_TRAIN_KERNEL", raising=False)
-        tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=N, steps=T,
+        tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
                      widths=widths, rng_state=x0)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
