@@ -39,19 +39,6 @@
 #ifndef XH_SV_ABL
 #define XH_SV_ABL 0
 #endif
-//   XH_SV_PF   1 = explicit one-step operand prefetch in layer 2 and dH1
-#ifndef XH_SV_PF
-#define XH_SV_PF 1
-#endif
-//   XH_SV_PF2  the same in dW2
-#ifndef XH_SV_PF2
-#define XH_SV_PF2 1
-#endif
-//   XH_SV_RM   1 = dH1's relu mask recomputed (two f32 MFMAs) instead of
-//              carried as a bit mask from layer 1
-#ifndef XH_SV_RM
-#define XH_SV_RM 1
-#endif
 
 namespace xh {
 namespace split {
@@ -198,7 +185,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   // (layer 1), the env's record (action, p_old, advantage: the loss).
   int bv[2][kD], iv[kD];
   bool item_a = true;  // of the group whose layer 1 ran last
-  unsigned maskT = 0u;  // bit 16 rt + j: H1[rt*32 + acc_row(j, h)][q*32 + lr] > 0
   auto fetch_rows = [&](int g) {
     const int t = g / N, e = g - t * N;
     const size_t ti = (size_t)t * N + e;
@@ -222,8 +208,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     float *xim = lf + F_X + p * (kD * 64);
     const float *b1f = lf + F_B1F + (item_a ? 0 : kH1);
     const float wa = lf[F_W1 + (q * 32 + lr) * kF0 + h];  // W1[i][k = h]
-    const float b1T = b1f[q * 32 + lr];
-    maskT = 0u;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       f32x16s t1 = lds_acc16(b1f, q * 32, h);
@@ -234,18 +218,9 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       const float xb = (float)(h == 0 ? xv0 : xv1) / (float)kCapacity;
       if (q == 0) xim[h * 64 + rt * 32 + lr] = xb;
       t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa, xb, t1, 0, 0, 0);
-#if !XH_SV_RM
-      f32x16s tT;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) tT[j] = b1T;
-      tT = __builtin_amdgcn_mfma_f32_32x32x2f32(xb, wa, tT, 0, 0, 0);
-#endif
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         t1[j] = relu(t1[j]);
-#if !XH_SV_RM
-        maskT |= (tT[j] > 0.0f ? 1u : 0u) << (16 * rt + j);
-#endif
       }
       img_store_split_b(h1i[0], h1i[1], h1i[2], rt == 0 ? sb0 : sb1, q * 32, t1);
     }
@@ -270,7 +245,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     }
     if (has_next) fetch_rows(gn);  // consumed by layer1() at the end
     const bool item_a_cur = item_a;
-    const unsigned mask_cur = maskT;
     const float *xim = lf + F_X + par * (kD * 64);
 
     // ---- layer 2 (H2 tile q, both r-tiles) + partial logits
@@ -279,7 +253,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       const int rb0 = opq(rb0_), rb1 = opq(rb1_), rbw = opq(rbw_);
       pre[0] = lds_acc16(lf + F_B2, q * 32, h);
       pre[1] = pre[0];
-#if XH_SV_PF
       // explicit one-step prefetch: step st = (K-slice st/2, r-tile st%2);
       // its operands are loaded while step st-1's MFMAs run
       bf16x8 lo_c = ld_row(w2lo, rbw, 0), lo_n = lo_c, b_c[3], b_n[3];
@@ -301,19 +274,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
         if (rt == 1) lo_c = lo_n;
       }
-#else
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8 wa[3] = {wl[s][0], wl[s][1], ld_row(w2lo, rbw, s)};
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          bf16x8 b[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p) b[p] = ld_row(h1i[p], rt == 0 ? rb0 : rb1, s);
-          if (!(XH_SV_ABL & 8)) pre[rt] = mfma_split6(wa, b, pre[rt]);
-        }
-      }
-#endif
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         float zp = 0.0f;
@@ -400,7 +360,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // ---- dW2 tiles (q, n), K = the 64 rows
     {
       const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
-#if XH_SV_PF2
       // explicit one-step prefetch over steps st = (K-slice st/4, tile st%4)
       bf16x8 a_c[3], a_n[3], b_c[3], b_n[3];
 #pragma unroll
@@ -428,22 +387,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           if (n == 3) a_c[p] = a_n[p];
         }
       }
-#else
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 af[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) af[p] = ld_tr(dai[p], tq0, tq1, s);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          bf16x8 bf[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            bf[p] = ld_tr(h1i[p], tb0 ^ (64 * n), tb1 ^ (64 * n), s);
-          if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split6(af, bf, accW2[n]);
-        }
-      }
-#endif
     }
     __syncthreads();  // H1 image consumed: the next group's layer 1 may write
 
@@ -460,7 +403,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         f32x16s dh;
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
-#if XH_SV_PF
         bf16x8 lo_c = ld_tr(w2lo, tq0, tq1, 0), lo_n = lo_c, b_c[3], b_n[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) b_c[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, 0);
@@ -478,18 +420,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
           lo_c = lo_n;
         }
-#else
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 wa[3] = {wd[s][0], wd[s][1], ld_tr(w2lo, tq0, tq1, s)};
-          bf16x8 b[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p) b[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s);
-          if (!(XH_SV_ABL & 4)) dh = mfma_split6(b, wa, dh);
-        }
-#endif
         if (XH_SV_ABL & 1) continue;
-#if XH_SV_RM
         // the transposed layer-1 tile again (the same two products as
         // layer1(): bit-identical), for relu' in this layout
         f32x16s tT;
@@ -502,7 +433,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
           for (int j = 0; j < 16; ++j) tT[j] = b1T;
           tT = __builtin_amdgcn_mfma_f32_32x32x2f32(xb, wa1, tT, 0, 0, 0);
         }
-#endif
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const float4 x0 = lds4(xim + rt * 32 + 8 * g4 + 4 * h);
@@ -512,11 +442,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int j = 4 * g4 + u;
-#if XH_SV_RM
             const float d = tT[j] > 0.0f ? dh[j] : 0.0f;
-#else
-            const float d = (mask_cur >> (16 * rt + j)) & 1u ? dh[j] : 0.0f;
-#endif
             sg += d;
             w0 = fmaf(d, xa[u], w0);
             w1 = fmaf(d, xc[u], w1);
