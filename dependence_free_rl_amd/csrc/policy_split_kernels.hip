@@ -1,8 +1,8 @@
 // policy_split_kernels.hip -- the PPO / actor-critic train epoch of the
-// 64-bin 2-D [128,128] policy (BASELINE configs 3 and 4) with its three
-// 128x128 GEMMs on the bf16 matrix cores at f32 accuracy (xh_split.h: each
-// f32 operand split exactly into three bf16 parts, six bf16 MFMAs per
-// K = 16 slice in place of eight f32 ones, 2.7x fewer MFMA cycles).
+// 64-bin 2-D [128,128] policy (BASELINE configs 3 and 4) and of the 128-bin
+// 3-D one (config 5) with their three 128x128 GEMMs on the bf16 matrix cores
+// at f32 accuracy (xh_split.h: each f32 operand split exactly into three
+// bf16 parts; six bf16 MFMAs per K = 16 slice in place of eight f32 ones).
 //
 // Same math as policy_train8_kernel (policy_kernels.hip): per 64-row group
 // (one env, its 64 bins) layer 1 (conv1d_1 F0 -> 128, item folded into the
@@ -12,20 +12,29 @@
 // dW2 = dA2^T H1, dH1 = dA2 W2 -> dA1 -> dW1 / db1 (nn.h:149-186).  One
 // gradient slab per workgroup, every entry written by exactly one wave.
 //
+// Rank-1 backward: layer 3 has one output per row, so
+//     dA2[r][o] = g_r w3_o M[r][o],   M = relu'(A2) in {0, 1},
+// and the two backward GEMMs run on the exact 0/1 image M (one bf16 part):
+//     dW2 = diag(w3) M^T (g (x) H1),   dH1 = diag(g) M W2',  W2' = diag(w3) W2
+// (g (x) H1 and W2' rounded once, split into three parts): three bf16 MFMAs
+// per K = 16 slice (xh_split.h mfma_split3) instead of six; w3 is applied to
+// dW2's tile at the write-out and g to dH1's rows in the dW1 sums.
+//
 // 4 waves (one per SIMD, 512 registers each), one workgroup per CU; wave q
 // owns 32-wide tile q of every product:
 //   layer 1: H1 tile q of both 32-row r-tiles -> split -> H1 image
 //   layer 2: H2 tile q (W2 row fragments in registers, H1 image rows),
 //            partial logits -> softmax + loss gradient (every wave, all rows)
-//   dA2 tile q -> split -> dA2 image; dW3 partial sums
-//   dH1 tile q = dA2 . W2[:, tile q] (W2^T fragments in registers, dA2
-//            image rows) -> relu' (bit mask) -> dW1 / db1 / item columns
+//   dW3 / db2 partial sums; M tile q -> the mask image, g (x) H1 tile q ->
+//            the H1 image (layer 2 has consumed it)
 //   dW2 tiles (q, 0..3) over the 64 rows (both operands by transposed image
-//            reads), db2 from the same dA2 fragments
-// Both sets of W2 hi / mid fragments (8 K-slices x 2 parts each, 128
-// registers) are loaded once per launch from split W2 images that the
-// prologue builds in the LDS the H1 / dA2 images use afterwards; W2's lo
-// part stays in an LDS image.
+//            reads)
+//   dH1 tile q = M . W2'[:, tile q] (W2'^T fragments in registers, mask
+//            image rows) -> relu' -> dW1 / db1 / item columns
+// The W2 hi / mid fragments of layer 2 and the W2' ones of dH1 (8 K-slices
+// x 2 parts each, 128 registers) are loaded once per launch from split
+// images that the prologue builds in the LDS the row images use afterwards;
+// the lo parts stay in LDS images (W2' lo in the mask region's spare parts).
 #include <cstdlib>
 
 #include "xh_device.h"
@@ -45,9 +54,9 @@ namespace split {
 
 constexpr int kB = 64, kD = 2, kF0 = 2 * kD, kH1 = 128, kH2 = 128;
 constexpr int kThreads = 256;
-// LDS carve (bytes): three part images of the 64-row H1 and dA2 tiles
-// ([row][feature], 256-byte swizzled rows), W2's lo-part image, then an f32
-// region.  The prologue's W2 hi / mid images (2 x 128 rows) alias the row
+// LDS carve (bytes): three part images of the 64-row H1 tile, the mask
+// image + W2' lo ([row][feature], 256-byte swizzled rows), W2's lo-part
+// image, then an f32 region.  The prologue's W2 hi / mid images (2 x 128 rows) alias the row
 // images; their fragments live in registers, the lo part's are read per use.
 constexpr int kImg = 64 * kImgRow;
 constexpr int L_H1 = 0, L_DA = 3 * kImg, L_W2 = 0;
@@ -60,7 +69,8 @@ constexpr int F_B3 = F_W3 + kH2;           // [4]
 constexpr int F_B1F = F_B3 + 4;            // [2][H1]: b1 + item part, per item
 constexpr int F_Z = F_B1F + 2 * kH1;       // [4][64] partial logits
 constexpr int F_X = F_Z + 4 * 64;          // [2 parity][2 dims][64 rows] bins/8
-constexpr int F_END = F_X + 2 * kD * 64;
+constexpr int F_G = F_X + 2 * kD * 64;     // [64] the rows' loss gradients
+constexpr int F_END = F_G + 64;
 // db2 partial sums per lane (dA2 summed over this lane's rows): [wave q][4]
 // [64 lanes] float4, read-modify-written once per group
 constexpr int L_B2A = L_F + sizeof(float) * F_END;
@@ -150,13 +160,33 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     for (int p = 0; p < 2; ++p) {
       const char *img = lds + L_W2 + p * 128 * kImgRow;
       wl[s][p] = ld_row(img, rbw_, s);
-      wd[s][p] = ld_tr(img, tq0_, tq1_, s);
     }
   __syncthreads();  // the W2 images' LDS becomes the row images
+  // W2' = diag(w3) W2 (rounded once), split: hi / mid images for dH1's
+  // fragments (the same LDS again), its lo image in the dA2 region's parts
+  // 1-2 (the mask needs one part)
+  for (int e = tid; e < kH2 * kH1; e += kThreads) {
+    const int o = e >> 7, i = e & 127;
+    __bf16 x0, x1, x2;
+    split3(P[PL.oW2() + e] * P[PL.ow3() + o], x0, x1, x2);
+    const int off = img_off(o, i >> 3) + 2 * (i & 7);
+    *reinterpret_cast<__bf16 *>(lds + L_W2 + off) = x0;
+    *reinterpret_cast<__bf16 *>(lds + L_W2 + 128 * kImgRow + off) = x1;
+    *reinterpret_cast<__bf16 *>(lds + L_DA + kImg + off) = x2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      wd[s][p] = ld_tr(lds + L_W2 + p * 128 * kImgRow, tq0_, tq1_, s);
+  __syncthreads();
 
   char *h1i[3] = {lds + L_H1, lds + L_H1 + kImg, lds + L_H1 + 2 * kImg};
-  char *dai[3] = {lds + L_DA, lds + L_DA + kImg, lds + L_DA + 2 * kImg};
+  char *mki = lds + L_DA;  // the 0/1 mask image M
   const char *w2lo = lds + L_W2LO;
+  // the lo part of dH1's operand W2' = diag(w3) W2
+  const char *w2dlo = lds + L_DA + kImg;
   const int N = a.b.N, T = a.b.T;
   const int ngroups = T * N;
 
@@ -348,44 +378,61 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
             b2[j] += d[j];
           }
         }
-        img_store_split_b(dai[0], dai[1], dai[2], rt == 0 ? sb0 : sb1, q * 32, d);
       }
+      if (q == 0) lf[F_G + lane] = gz;
 #pragma unroll
       for (int j4 = 0; j4 < 4; ++j4)
         b2acc[64 * j4] = make_float4(b2[4 * j4], b2[4 * j4 + 1], b2[4 * j4 + 2],
                                      b2[4 * j4 + 3]);
+      // the backward GEMMs' operands: relu'(A2) as an exact 0/1 image (one
+      // bf16 part) and g (x) H1 (the layer-1 tile again, bit-identical to
+      // layer1()'s, times the row's gradient: three parts, over the H1 image,
+      // which every wave's layer 2 has read before the logits barrier)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const float gr = h == rt ? gz : sw;
+        const int sbb = rt == 0 ? sb0 : sb1;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          bf16x4 mk;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            mk[u] = pre[rt][4 * g4 + u] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
+          *reinterpret_cast<bf16x4 *>(mki + (sbb ^ (16 * (4 * q + g4)))) = mk;
+        }
+        const float *b1f = lf + F_B1F + (item_a_cur ? 0 : kH1);
+        f32x16s t1 = lds_acc16(b1f, q * 32, h);
+        t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(
+            lf[F_W1 + (q * 32 + lr) * kF0 + h], xim[h * 64 + rt * 32 + lr], t1, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t1[j] = relu(t1[j]) * gr;
+        img_store_split_b(h1i[0], h1i[1], h1i[2], sbb, q * 32, t1);
+      }
     }
     __syncthreads();
 
-    // ---- dW2 tiles (q, n), K = the 64 rows
+    // ---- dW2 tiles (q, n) / w3, K = the 64 rows: M^T (g (x) H1)
     {
       const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
       // explicit one-step prefetch over steps st = (K-slice st/4, tile st%4)
-      bf16x8 a_c[3], a_n[3], b_c[3], b_n[3];
+      bf16x8 m_c = ld_tr(mki, tq0, tq1, 0), m_n = m_c, b_c[3], b_n[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        a_c[p] = ld_tr(dai[p], tq0, tq1, 0);
-        b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
-        a_n[p] = a_c[p];
-      }
+      for (int p = 0; p < 3; ++p) b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
         const int n = st & 3;
         if (st + 1 < 16) {
           const int s1 = (st + 1) >> 2, n1 = (st + 1) & 3;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) {
+          for (int p = 0; p < 3; ++p)
             b_n[p] = ld_tr(h1i[p], tb0 ^ (64 * n1), tb1 ^ (64 * n1), s1);
-            if (n1 == 0) a_n[p] = ld_tr(dai[p], tq0, tq1, s1);
-          }
+          if (n1 == 0) m_n = ld_tr(mki, tq0, tq1, s1);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split6(a_c, b_c, accW2[n]);
+        if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split3(m_c, b_c, accW2[n]);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          b_c[p] = b_n[p];
-          if (n == 3) a_c[p] = a_n[p];
-        }
+        for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+        if (n == 3) m_c = m_n;
       }
     }
     __syncthreads();  // H1 image consumed: the next group's layer 1 may write
@@ -403,21 +450,19 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         f32x16s dh;
 #pragma unroll
         for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
-        bf16x8 lo_c = ld_tr(w2lo, tq0, tq1, 0), lo_n = lo_c, b_c[3], b_n[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b_c[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, 0);
+        const int rb = rt == 0 ? rb0 : rb1;
+        bf16x8 lo_c = ld_tr(w2dlo, tq0, tq1, 0), lo_n = lo_c;
+        bf16x8 m_c = ld_row(mki, rb, 0), m_n = m_c;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           if (s + 1 < 8) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) b_n[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s + 1);
-            lo_n = ld_tr(w2lo, tq0, tq1, s + 1);
+            m_n = ld_row(mki, rb, s + 1);
+            lo_n = ld_tr(w2dlo, tq0, tq1, s + 1);
           }
           __builtin_amdgcn_sched_barrier(0);
           const bf16x8 wa[3] = {wd[s][0], wd[s][1], lo_c};
-          if (!(XH_SV_ABL & 4)) dh = mfma_split6(b_c, wa, dh);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+          if (!(XH_SV_ABL & 4)) dh = mfma_split3(m_c, wa, dh);
+          m_c = m_n;
           lo_c = lo_n;
         }
         if (XH_SV_ABL & 1) continue;
@@ -435,14 +480,18 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
         }
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
+          // dH1 = g_r (M W2')[r][i] (registers = rows rt*32 + acc_row(j, h)):
+          // g_r is applied through the rows' g, g x0, g x1
           const float4 x0 = lds4(xim + rt * 32 + 8 * g4 + 4 * h);
           const float4 x1 = lds4(xim + 64 + rt * 32 + 8 * g4 + 4 * h);
+          const float4 gg = lds4(lf + F_G + rt * 32 + 8 * g4 + 4 * h);
+          const float gv[4] = {gg.x, gg.y, gg.z, gg.w};
           const float xa[4] = {x0.x, x0.y, x0.z, x0.w};
           const float xc[4] = {x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int j = 4 * g4 + u;
-            const float d = tT[j] > 0.0f ? dh[j] : 0.0f;
+            const float d = tT[j] > 0.0f ? dh[j] * gv[u] : 0.0f;
             sg += d;
             w0 = fmaf(d, xa[u], w0);
             w1 = fmaf(d, xc[u], w1);
@@ -466,7 +515,8 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] = accW2[n][j];
+      slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] =
+          accW2[n][j] * lf[F_W3 + q * 32 + acc_row(j, h)];
   {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -529,7 +579,8 @@ constexpr int F_B3 = F_W3 + kH2;         // [4]
 constexpr int F_B1F = F_B3 + 4;          // [2][H1]
 constexpr int F_Z = F_B1F + 2 * kH1;     // [4][128] partial logits
 constexpr int F_X = F_Z + 4 * 128;       // [3 dims][64 rows] of the current half
-constexpr int F_END = F_X + kD * 64;
+constexpr int F_G = F_X + kD * 64;       // [64] the half's row gradients
+constexpr int F_END = F_G + 64;
 constexpr int L_B2A = L_F + sizeof(float) * F_END;
 constexpr size_t kLds = L_B2A + 4 * 4 * 64 * 16;
 static_assert(kLds <= 160 * 1024, "LDS");
@@ -544,7 +595,7 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
                 L_W2LO = s128::L_W2LO, L_F = s128::L_F, L_B2A = s128::L_B2A;
   constexpr int F_W1 = s128::F_W1, F_B2 = s128::F_B2, F_W3 = s128::F_W3,
                 F_B3 = s128::F_B3, F_B1F = s128::F_B1F, F_Z = s128::F_Z,
-                F_X = s128::F_X;
+                F_X = s128::F_X, F_G = s128::F_G;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
   const PolicyLayout PL{kF0, kH1, kH2};
@@ -594,13 +645,30 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     for (int p = 0; p < 2; ++p) {
       const char *img = lds + L_W2 + p * 128 * kImgRow;
       wl[s][p] = ld_row(img, rbw_, s);
-      wd[s][p] = ld_tr(img, tq0_, tq1_, s);
     }
+  __syncthreads();
+  // W2' = diag(w3) W2 for dH1 (as the 64-row kernel)
+  for (int e = tid; e < kH2 * kH1; e += kThreads) {
+    const int o = e >> 7, i = e & 127;
+    __bf16 x0, x1, x2;
+    split3(P[PL.oW2() + e] * P[PL.ow3() + o], x0, x1, x2);
+    const int off = img_off(o, i >> 3) + 2 * (i & 7);
+    *reinterpret_cast<__bf16 *>(lds + L_W2 + off) = x0;
+    *reinterpret_cast<__bf16 *>(lds + L_W2 + 128 * kImgRow + off) = x1;
+    *reinterpret_cast<__bf16 *>(lds + L_DA + kImg + off) = x2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      wd[s][p] = ld_tr(lds + L_W2 + p * 128 * kImgRow, tq0_, tq1_, s);
   __syncthreads();
 
   char *h1i[3] = {lds + L_H1, lds + L_H1 + kImg, lds + L_H1 + 2 * kImg};
-  char *dai[3] = {lds + L_DA, lds + L_DA + kImg, lds + L_DA + 2 * kImg};
+  char *mki = lds + L_DA;  // the 0/1 mask image M
   const char *w2lo = lds + L_W2LO;
+  const char *w2dlo = lds + L_DA + kImg;  // W2' lo
   float *xim = lf + F_X;
   const int N = a.b.N, T = a.b.T;
   const int ngroups = T * N;
@@ -709,8 +777,10 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
       if (lane < 32) lf[F_Z + q * 128 + hg * 64 + rt * 32 + lr] = zp;
     }
   };
-  // ---- dA2 tile q of one half (row gradients gz: lane = row of the half)
-  auto dA2 = [&](const f32x16s (&pre)[2], float gz) {
+  // ---- dA2 of one half (row gradients gz: lane = row of the half): dW3,
+  // db2, and the backward GEMMs' operands (the 64-row kernel's rank-1 form):
+  // the 0/1 relu'(A2) image and g (x) H1 over the H1 image of half hg
+  auto dA2 = [&](const f32x16s (&pre)[2], float gz, int hg, bool item_a) {
     const float sw = half_swap(gz);
     float b2[16];
 #pragma unroll
@@ -738,41 +808,55 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
           b2[j] += d[j];
         }
       }
-      img_store_split_b(dai[0], dai[1], dai[2], rt == 0 ? sb0 : sb1, q * 32, d);
     }
+    if (q == 0) lf[F_G + lane] = gz;
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4)
       b2acc[64 * j4] = make_float4(b2[4 * j4], b2[4 * j4 + 1], b2[4 * j4 + 2],
                                    b2[4 * j4 + 3]);
+    const float *b1f = lf + F_B1F + (item_a ? 0 : kH1);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const float gr = h == rt ? gz : sw;
+      const int sbb = rt == 0 ? sb0 : sb1;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 mk;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          mk[u] = pre[rt][4 * g4 + u] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
+        *reinterpret_cast<bf16x4 *>(mki + (sbb ^ (16 * (4 * q + g4)))) = mk;
+      }
+      f32x16s t1 = lds_acc16(b1f, q * 32, h);
+#pragma unroll
+      for (int s1 = 0; s1 < kS1; ++s1)
+        t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w1k(s1), xfeat(hg, rt, s1), t1, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t1[j] = relu(t1[j]) * gr;
+      img_store_split_b(h1i[0], h1i[1], h1i[2], sbb, q * 32, t1);
+    }
   };
-  // ---- dW2 tiles (q, n) over the imaged half's 64 rows
+  // ---- dW2 tiles (q, n) / w3 over the imaged half's 64 rows: M^T (g (x) H1)
   auto dW2 = [&]() {
     const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
-    bf16x8 a_c[3], a_n[3], b_c[3], b_n[3];
+    bf16x8 m_c = ld_tr(mki, tq0, tq1, 0), m_n = m_c, b_c[3], b_n[3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      a_c[p] = ld_tr(dai[p], tq0, tq1, 0);
-      b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
-      a_n[p] = a_c[p];
-    }
+    for (int p = 0; p < 3; ++p) b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       const int n = st & 3;
       if (st + 1 < 16) {
         const int s1 = (st + 1) >> 2, n1 = (st + 1) & 3;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < 3; ++p)
           b_n[p] = ld_tr(h1i[p], tb0 ^ (64 * n1), tb1 ^ (64 * n1), s1);
-          if (n1 == 0) a_n[p] = ld_tr(dai[p], tq0, tq1, s1);
-        }
+        if (n1 == 0) m_n = ld_tr(mki, tq0, tq1, s1);
       }
       __builtin_amdgcn_sched_barrier(0);
-      accW2[n] = mfma_split6(a_c, b_c, accW2[n]);
+      accW2[n] = mfma_split3(m_c, b_c, accW2[n]);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        b_c[p] = b_n[p];
-        if (n == 3) a_c[p] = a_n[p];
-      }
+      for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+      if (n == 3) m_c = m_n;
     }
   };
   // ---- dH1 tile q of the half (transposed) -> relu' -> dW1 / db1 / items
@@ -786,21 +870,19 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
       f32x16s dh;
 #pragma unroll
       for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
-      bf16x8 lo_c = ld_tr(w2lo, tq0, tq1, 0), lo_n = lo_c, b_c[3], b_n[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) b_c[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, 0);
+      const int rb = rt == 0 ? rb0 : rb1;
+      bf16x8 lo_c = ld_tr(w2dlo, tq0, tq1, 0), lo_n = lo_c;
+      bf16x8 m_c = ld_row(mki, rb, 0), m_n = m_c;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         if (s + 1 < 8) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p) b_n[p] = ld_row(dai[p], rt == 0 ? rb0 : rb1, s + 1);
-          lo_n = ld_tr(w2lo, tq0, tq1, s + 1);
+          m_n = ld_row(mki, rb, s + 1);
+          lo_n = ld_tr(w2dlo, tq0, tq1, s + 1);
         }
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 wa[3] = {wd[s][0], wd[s][1], lo_c};
-        dh = mfma_split6(b_c, wa, dh);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
+        dh = mfma_split3(m_c, wa, dh);
+        m_c = m_n;
         lo_c = lo_n;
       }
       // the transposed layer-1 tile (the same two-step chain as layer1())
@@ -821,10 +903,13 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
         const float xa[4] = {x0.x, x0.y, x0.z, x0.w};
         const float xc[4] = {x1.x, x1.y, x1.z, x1.w};
         const float xe[4] = {x2.x, x2.y, x2.z, x2.w};
+        // dH1 = g_r (M W2')[r][i]: registers are rows rt*32 + acc_row(j, h)
+        const float4 gg = lds4(lf + F_G + rt * 32 + 8 * g4 + 4 * h);
+        const float gv[4] = {gg.x, gg.y, gg.z, gg.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int j = 4 * g4 + u;
-          const float d = tT[j] > 0.0f ? dh[j] : 0.0f;
+          const float d = tT[j] > 0.0f ? dh[j] * gv[u] : 0.0f;
           sg += d;
           wf0 = fmaf(d, xa[u], wf0);
           wf1 = fmaf(d, xc[u], wf1);
@@ -918,8 +1003,9 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
         layer1(0, item_a);
         __syncthreads();
         layer2(pre);
+        __syncthreads();  // dA2 overwrites the H1 image layer 2 reads
       }
-      dA2(pre, hb == 0 ? gz1 : gz0);
+      dA2(pre, hb == 0 ? gz1 : gz0, hb == 0 ? 1 : 0, item_a);
       __syncthreads();
       dW2();
       __syncthreads();
@@ -933,7 +1019,8 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] = accW2[n][j];
+      slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] =
+          accW2[n][j] * lf[F_W3 + q * 32 + acc_row(j, h)];
   if (q == 0) {
     float v3 = accB3;
 #pragma unroll

@@ -67,6 +67,16 @@ __device__ __forceinline__ f32x16s mfma_split6(const bf16x8 (&a)[3],
   return c;
 }
 
+// An operand that is exact in bf16 (e.g. a 0/1 mask) times a split one:
+// three products, error <= 2^-24 sum|a_k b_k| (the split's e term only).
+__device__ __forceinline__ f32x16s mfma_split3(bf16x8 a, const bf16x8 (&b)[3],
+                                               f32x16s c) {
+  c = mfma_bf16(a, b[2], c);
+  c = mfma_bf16(a, b[1], c);
+  c = mfma_bf16(a, b[0], c);
+  return c;
+}
+
 // Row read: the 8 bf16 of chunk ch of row `row` of an image.
 __device__ __forceinline__ bf16x8 img_row8(const char *img, int row, int ch) {
   return *reinterpret_cast<const bf16x8 *>(img + img_off(row, ch));
