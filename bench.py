@@ -62,6 +62,11 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 # in f32-equivalent FLOP/s is the dense bf16 peak (MI355X_MICROARCH.md,
 # ~2.5 PFLOP/s) / 6.
 SPLIT_PEAK_TFLOPS = 2500.0 / 6
+# The split train kernels' two backward GEMMs take the exact 0/1 relu mask as
+# one operand (rank-1 backward): three bf16 products per f32
+# product there, six in layer 2 -- equal FLOPs each, so (6 + 3 + 3) / 3 = 4
+# bf16 products per f32-equivalent FLOP on average: peak = dense bf16 / 4.
+TRAIN_SPLIT_PEAK_TFLOPS = 2500.0 / 4
 
 
 def rollout_split_active():
@@ -291,7 +296,7 @@ def main():
     split_name = ("policy_train_split128" if B == 128 else "policy_train_split_kernel")
     traffic, traffic_src, pmc = (pmc_traffic(split_name, any_shape=True)
                                  if split else pmc_traffic())
-    train_peak = SPLIT_PEAK_TFLOPS if split else FP32_PEAK_TFLOPS
+    train_peak = TRAIN_SPLIT_PEAK_TFLOPS if split else FP32_PEAK_TFLOPS
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
@@ -348,8 +353,9 @@ def main():
                    "lr_scale_rows": not args.reference_lr},
         "roofline": {"kernel": "policy_train", "bound": "mfma",
                      "math": ("f32 operands split exactly into 3 bf16 parts, "
-                              "6 bf16 MFMA products per f32 product, f32 "
-                              "accumulate; peak = dense bf16 peak / 6"
+                              "f32 accumulate: layer 2 6 bf16 MFMA products per "
+                              "f32 product, dW2 / dH1 3 (exact 0/1 relu-mask "
+                              "operand); peak = dense bf16 peak / 4"
                               if split else "f32 MFMA (v_mfma_f32_32x32x2_f32)"),
                      "achieved": round(achieved, 2), "peak": round(train_peak, 1),
                      "unit": "TFLOP/s",
