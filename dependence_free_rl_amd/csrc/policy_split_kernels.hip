@@ -27,8 +27,8 @@
 //            partial logits -> softmax + loss gradient (every wave, all rows)
 //   dW3 / db2 partial sums; M tile q -> the mask image, g (x) H1 tile q ->
 //            the H1 image (layer 2 has consumed it)
-//   dW2 tiles (q, 0..3) over the 64 rows (both operands by transposed image
-//            reads)
+//   dW2 tiles (0..3, q) over the 64 rows (both operands by transposed image
+//            reads; i-tile q of g (x) H1 held per K-half, the mask streamed)
 //   dH1 tile q = M . W2'[:, tile q] (W2'^T fragments in registers, mask
 //            image rows) -> relu' -> dW1 / db1 / item columns
 // The W2 hi / mid fragments of layer 2 and the W2' ones of dH1 (8 K-slices
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   const int N = a.b.N, T = a.b.T;
   const int ngroups = T * N;
 
-  // dW2 tiles (q, n); dW3 partial sums (lane = row layout); dW1 of feature
+  // dW2 tiles (n, q); dW3 partial sums (lane = row layout); dW1 of feature
   // i = q*32 + lr over this lane half's rows: bin columns w0 / w1 and the dA1
   // sums over rows holding item_a / item_b (the item columns and db1)
   f32x16s accW2[4];
@@ -411,28 +411,31 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     }
     __syncthreads();
 
-    // ---- dW2 tiles (q, n) / w3, K = the 64 rows: M^T (g (x) H1)
+    // ---- dW2 tiles (n, q) / w3, K = the 64 rows: M^T (g (x) H1).  Wave q's
+    // B operand (i-tile q of g (x) H1, three parts) is loaded once per
+    // K-half and reused over the four o-tiles of the mask (one part):
+    // 28 KB of LDS reads per wave instead of 52
     {
       const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
-      // explicit one-step prefetch over steps st = (K-slice st/4, tile st%4)
-      bf16x8 m_c = ld_tr(mki, tq0, tq1, 0), m_n = m_c, b_c[3], b_n[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b_c[p] = ld_tr(h1i[p], tb0, tb1, 0);
+      for (int kh = 0; kh < 2; ++kh) {
+        bf16x8 bq[2][3];
 #pragma unroll
-      for (int st = 0; st < 16; ++st) {
-        const int n = st & 3;
-        if (st + 1 < 16) {
-          const int s1 = (st + 1) >> 2, n1 = (st + 1) & 3;
+        for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-          for (int p = 0; p < 3; ++p)
-            b_n[p] = ld_tr(h1i[p], tb0 ^ (64 * n1), tb1 ^ (64 * n1), s1);
-          if (n1 == 0) m_n = ld_tr(mki, tq0, tq1, s1);
+          for (int p = 0; p < 3; ++p) bq[ss][p] = ld_tr(h1i[p], tq0, tq1, 2 * kh + ss);
+        bf16x8 m_c = ld_tr(mki, tb0, tb1, 2 * kh), m_n = m_c;
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const int n = st >> 1, ss = st & 1;
+          if (st + 1 < 8) {
+            const int n1 = (st + 1) >> 1, s1 = (st + 1) & 1;
+            m_n = ld_tr(mki, tb0 ^ (64 * n1), tb1 ^ (64 * n1), 2 * kh + s1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split3(m_c, bq[ss], accW2[n]);
+          m_c = m_n;
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (!(XH_SV_ABL & 2)) accW2[n] = mfma_split3(m_c, b_c, accW2[n]);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
-        if (n == 3) m_c = m_n;
       }
     }
     __syncthreads();  // H1 image consumed: the next group's layer 1 may write
@@ -515,8 +518,8 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      slab[PL.oW2() + (q * 32 + acc_row(j, h)) * kH1 + n * 32 + lr] =
-          accW2[n][j] * lf[F_W3 + q * 32 + acc_row(j, h)];
+      slab[PL.oW2() + (n * 32 + acc_row(j, h)) * kH1 + q * 32 + lr] =
+          accW2[n][j] * lf[F_W3 + n * 32 + acc_row(j, h)];
   {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -837,6 +840,7 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     }
   };
   // ---- dW2 tiles (q, n) / w3 over the imaged half's 64 rows: M^T (g (x) H1)
+  // (the 64-row kernel's (n, q) tiling measured 0.8% slower here)
   auto dW2 = [&]() {
     const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
     bf16x8 m_c = ld_tr(mki, tq0, tq1, 0), m_n = m_c, b_c[3], b_n[3];
