@@ -285,12 +285,16 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                hipStream_t s);
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                int grid, hipStream_t s);
-// The f32-accurate bf16-split train kernel (policy_split_kernels.hip) for the
-// 64-bin 2-D [128,128] shape; XH_TRAIN_KERNEL=f32 selects the f32-MFMA one.
+// The f32-accurate bf16-split train kernels for the 64-bin 2-D
+// (policy_split_kernels.hip) and 128-bin 3-D (policy_split128_kernels.hip)
+// [128,128] shapes; XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.
+constexpr int kSplit128Bins = 128, kSplit128Dims = 3;
 bool train_split_enabled();
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2);
 hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
                                      hipStream_t s);
+hipError_t launch_policy_train_split128(const PolicyTrainArgs &a, int grid,
+                                        hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
                               hipStream_t s);

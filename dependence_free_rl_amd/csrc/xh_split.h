@@ -193,4 +193,31 @@ __device__ __forceinline__ void img_store_split(char *img_hi, char *img_mid,
   }
 }
 
+// ---- helpers of the split train kernels (policy_split_kernels.hip,
+// policy_split128_kernels.hip)
+namespace split {
+
+__device__ __forceinline__ float relu(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+__device__ __forceinline__ float4 lds4(const float *p) {
+  return *reinterpret_cast<const float4 *>(p);
+}
+// 16 f32 of C-layout register order from 4 consecutive-feature quads of an
+// LDS vector: register 4g + u = v[c0 + 8g + 4h + u]
+__device__ __forceinline__ f32x16s lds_acc16(const float *v, int c0, int h) {
+  f32x16s r;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 b = lds4(v + c0 + 8 * g + 4 * h);
+    r[4 * g + 0] = b.x;
+    r[4 * g + 1] = b.y;
+    r[4 * g + 2] = b.z;
+    r[4 * g + 3] = b.w;
+  }
+  return r;
+}
+
+}  // namespace split
+
 }  // namespace xh
