@@ -73,7 +73,7 @@ constexpr int F_Z = F_B1F + 2 * kH1;       // [4][64] partial logits
 constexpr int F_X = F_Z + 4 * 64;          // [2 parity][2 dims][64 rows] bins/8
 constexpr int F_G = F_X + 2 * kD * 64;     // [64] the rows' loss gradients
 constexpr int F_END = F_G + 64;
-// db2 partial sums per lane (dA2 summed over this lane's rows): [wave q][4]
+// db2 / w3 partial sums per lane (g M summed over this lane's rows): [wave q][4]
 // [64 lanes] float4, read-modify-written once per group
 constexpr int L_B2A = L_F + sizeof(float) * F_END;
 constexpr size_t kLds = L_B2A + 4 * 4 * 64 * 16;
@@ -345,19 +345,13 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
       for (int rt = 0; rt < 2; ++rt) {
         // row rt*32 + lr's gradient: own lane in half rt, else lane ^ 32
         const float gr = h == rt ? gz : sw;
-        f32x16s d;
+        // dW3 partial sums; db2 / w3 = sum_r g_r M[r][o] (w3 applied at the
+        // write-out, as dW2's)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 ww = lds4(lf + F_W3 + q * 32 + 8 * g4 + 4 * h);
-          const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int j = 4 * g4 + u;
-            const float v = pre[rt][j];
-            accW3[j] += gr * relu(v);
-            d[j] = v > 0.0f ? gr * wq[u] : 0.0f;
-            b2[j] += d[j];
-          }
+        for (int j = 0; j < 16; ++j) {
+          const float v = pre[rt][j];
+          accW3[j] += gr * relu(v);
+          b2[j] += v > 0.0f ? gr : 0.0f;
         }
       }
       if (q == 0) lf[F_G + lane] = gz;
@@ -506,7 +500,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     for (int j = 0; j < 16; ++j) {
       // db2: sums over the 32 rows of each lane half (valid in lr >= 16)
       const float s2 = half_sum32(b2acc[64 * (j >> 2)][j & 3]);
-      if (lr == 31) slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2;
+      if (lr == 31) slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2 * lf[F_W3 + q * 32 + acc_row(j, h)];
     }
   }
   if (q == 0) {
