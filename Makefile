@@ -36,9 +36,11 @@ all: lib oracle compat
 lib: $(LIB)
 
 # per-file code-generation flags, measured per kernel: the
-# 64-row split train kernel with the VGPR form of the MFMAs (no spills,
-# 8% faster); the 128-row one is 2% slower with it and keeps the default
+# split train kernels with the VGPR form of the MFMAs (the accumulators need
+# not live in AGPRs: 64-row kernel 0 B of spills and 8% faster; the 128-row
+# one keeps half 0's pre-activations in registers with it, 6% faster)
 FLAGS_policy_split_kernels := -mllvm -amdgpu-mfma-vgpr-form
+FLAGS_policy_split128_kernels := -mllvm -amdgpu-mfma-vgpr-form
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@

@@ -2,8 +2,7 @@
 // config 5) on the split GEMMs with the rank-1 backward: the math and the
 // image layout of policy_split_kernels.hip (see its header), one env of 128
 // rows per group.  A file of its own so that each kernel is compiled with
-// the flags measured best for it (Makefile: the 64-row kernel with the VGPR
-// form of the MFMAs; this one without: +2% with it).
+// the flags measured best for it (Makefile).
 #include "xh_device.h"
 #include "xh_kernels.h"
 #include "xh_split.h"
@@ -13,12 +12,13 @@ namespace split {
 
 // ============================== 128 bins, 3-D (BASELINE config 5), AC/PPO ==
 // The same split GEMMs for one env of 128 rows per group = two 64-row
-// half-groups through the 64-row images: layer 1 + layer 2 of half 0 (logits
-// only), of half 1 (its pre-activations kept), the softmax over all 128 bins,
-// the backward of half 1, then half 0's layer 1 and layer 2 recomputed (its
-// H1 image and pre-activations cannot stay beside half 1's: the recompute is
-// the same code, bit-identical) and its backward.  Layer 1 runs 2 k-steps
-// (D = 3 bin features, the item folded into the bias).
+// half-groups through the 64-row images: layer 1 + layer 2 of half 0 and of
+// half 1 (both halves' pre-activations kept in registers), the softmax over
+// all 128 bins, the backward of half 1, then of half 0: the backward needs
+// no H1 image of its own (dA2 writes g (x) H1 from the layer-1 tile
+// recomputed from the bins, bit-identical), so only the X image is
+// rewritten.  Layer 1 runs 2 k-steps (D = 3 bin features, the item folded
+// into the bias).
 namespace s128 {
 constexpr int kB = 128, kD = 3, kF0 = 2 * kD, kH1 = 128, kH2 = 128, kS1 = 2;
 constexpr int kThreads = 256;
@@ -393,13 +393,17 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     }
 
     // ---- forward: half 0 (logits only), half 1 (pre kept)
-    f32x16s pre[2];
+    f32x16s pre[2], pre0[2];
 #pragma unroll 1
     for (int hg = 0; hg < 2; ++hg) {
       layer1(hg, item_a);
       __syncthreads();
       layer2(pre);
       logits(pre, hg);
+      if (hg == 0) {
+        pre0[0] = pre[0];
+        pre0[1] = pre[1];
+      }
       __syncthreads();
     }
 
@@ -455,10 +459,17 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
 #pragma unroll 1
     for (int hb = 0; hb < 2; ++hb) {
       if (hb == 1) {
-        layer1(0, item_a);
-        __syncthreads();
-        layer2(pre);
-        __syncthreads();  // dA2 overwrites the H1 image layer 2 reads
+        // half 0's pre-activations were kept; dA2 rebuilds its g (x) H1
+        // image from the bins, dH1 reads its X image
+        pre[0] = pre0[0];
+        pre[1] = pre0[1];
+        if (q == 0) {
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) {
+            xim[h * 64 + rt * 32 + lr] = xfeat(0, rt, 0);
+            if (h == 0) xim[2 * 64 + rt * 32 + lr] = xfeat(0, rt, 1);
+          }
+        }
       }
       dA2(pre, hb == 0 ? gz1 : gz0, hb == 0 ? 1 : 0, item_a);
       __syncthreads();
