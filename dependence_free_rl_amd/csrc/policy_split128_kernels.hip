@@ -248,19 +248,13 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       const float gr = h == rt ? gz : sw;
-      f32x16s d;
+      // dW3 partial sums; db2 / w3 = sum_r g_r M[r][o] (w3 applied at the
+      // write-out, as dW2's)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 ww = lds4(lf + F_W3 + q * 32 + 8 * g4 + 4 * h);
-        const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = 4 * g4 + u;
-          const float v = pre[rt][j];
-          accW3[j] += gr * relu(v);
-          d[j] = v > 0.0f ? gr * wq[u] : 0.0f;
-          b2[j] += d[j];
-        }
+      for (int j = 0; j < 16; ++j) {
+        const float v = pre[rt][j];
+        accW3[j] += gr * relu(v);
+        b2[j] += v > 0.0f ? gr : 0.0f;
       }
     }
     if (q == 0) lf[F_G + lane] = gz;
@@ -498,7 +492,7 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     const float s2 = half_sum32(b2acc[64 * (j >> 2)][j & 3]);
     const float s3 = half_sum32(accW3[j]);
     if (lr == 31) {
-      slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2;
+      slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2 * lf[F_W3 + q * 32 + acc_row(j, h)];
       slab[PL.ow3() + q * 32 + acc_row(j, h)] = s3;
     }
   }
