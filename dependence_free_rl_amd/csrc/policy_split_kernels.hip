@@ -127,13 +127,6 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
   const int tb0_ = tr_base(lane, 0), tb1_ = tr_base(lane, 1);
   const int tq0_ = tb0_ ^ (64 * q), tq1_ = tb1_ ^ (64 * q);
   const int sb0 = st_base(lr, h), sb1 = st_base(32 + lr, h);
-  // Opaque copies per phase: the XORs with the compile-time slice / tile
-  // offsets are then issued where the reads are (one v_xor each) instead of
-  // being hoisted out of the group loop into ~40 extra live registers.
-  auto opq = [](int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-  };
   bf16x8 wl[8][2], wd[8][2];
 #pragma unroll
   for (int s = 0; s < 8; ++s)
@@ -261,7 +254,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // ---- layer 2 (H2 tile q, both r-tiles) + partial logits
     f32x16s pre[2];
     {
-      const int rb0 = opq(rb0_), rb1 = opq(rb1_), rbw = opq(rbw_);
+      const int rb0 = rb0_, rb1 = rb1_, rbw = rbw_;
       pre[0] = lds_acc16(lf + F_B2, q * 32, h);
       pre[1] = pre[0];
       // explicit one-step prefetch: step st = (K-slice st/2, r-tile st%2);
@@ -391,7 +384,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // K-half and reused over the four o-tiles of the mask (one part):
     // 28 KB of LDS reads per wave instead of 52
     {
-      const int tb0 = opq(tb0_), tb1 = opq(tb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
+      const int tb0 = tb0_, tb1 = tb1_, tq0 = tq0_, tq1 = tq1_;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         bf16x8 bq[2][3];
@@ -421,7 +414,7 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
     // r-tile by r-tile, so r-tile 0's VALU overlaps r-tile 1's MFMAs.  Layer
     // 1 of the next group in the same phase.
     {
-      const int rb0 = opq(rb0_), rb1 = opq(rb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
+      const int rb0 = rb0_, rb1 = rb1_, tq0 = tq0_, tq1 = tq1_;
       float sg = 0.0f;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
