@@ -13,7 +13,8 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/policy_split_kernels.o \
-            $(SRC)/policy_split128_kernels.o $(SRC)/xylo_hip.o
+            $(SRC)/policy_split128_kernels.o $(SRC)/policy_split8w_kernels.o \
+            $(SRC)/xylo_hip.o
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
@@ -41,6 +42,7 @@ lib: $(LIB)
 # one keeps half 0's pre-activations in registers with it, 6% faster)
 FLAGS_policy_split_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split128_kernels := -mllvm -amdgpu-mfma-vgpr-form
+FLAGS_policy_split8w_kernels := -mllvm -amdgpu-mfma-vgpr-form
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@
@@ -67,7 +69,7 @@ oracle:
 
 # test programs of the drop-in layer (tests/compat), prebuilt so the GPU box
 # runs them without a compiler step
-COMPAT_TESTS := $(COMPAT)/bound_env_by_hand
+COMPAT_TESTS := $(COMPAT)/bound_env_by_hand $(COMPAT)/save_weights
 
 compat: $(EXAMPLES) $(COMPAT_TESTS)
 	@mkdir -p $(COMPAT)
@@ -78,6 +80,10 @@ compat: $(EXAMPLES) $(COMPAT_TESTS)
 	  done; fi
 
 $(COMPAT)/bound_env_by_hand: tests/compat/bound_env_by_hand.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
+
+$(COMPAT)/save_weights: tests/compat/save_weights.cc $(COMPAT_HDRS) $(LIB)
 	@mkdir -p $(COMPAT)
 	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
 

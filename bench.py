@@ -56,36 +56,28 @@ def select_config(c):
     F0, ALGO, EPOCHS, REF_ITERS = 2 * D, k["algo"], k["epochs"], k["ref_iters"]
     return k
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
-# The config-3/4 train kernel (csrc/policy_split_kernels.hip) runs its GEMMs
-# on the bf16 matrix cores at f32 accuracy: every f32 product as six bf16
-# products of the operands' exact three-part splits, so its MFMA-bound peak
-# in f32-equivalent FLOP/s is the dense bf16 peak (MI355X_MICROARCH.md,
-# ~2.5 PFLOP/s) / 6.
-SPLIT_PEAK_TFLOPS = 2500.0 / 6
-# The split train kernels' two backward GEMMs take the exact 0/1 relu mask as
-# one operand (rank-1 backward): three bf16 products per f32
-# product there, six in layer 2 -- equal FLOPs each, so (6 + 3 + 3) / 3 = 4
-# bf16 products per f32-equivalent FLOP on average: peak = dense bf16 / 4.
-TRAIN_SPLIT_PEAK_TFLOPS = 2500.0 / 4
-
-
-def rollout_split_active():
-    """Mirrors rollout_split() in csrc/policy_kernels.hip: the 64-bin 2-D
-    and 128-bin 3-D [128,128] rollouts run layer 2 on the bf16-split GEMM
-    unless XH_ROLLOUT_KERNEL is f32 or 4."""
-    e = os.environ.get("XH_ROLLOUT_KERNEL", "")
-    return ((B, D, H1, H2) in ((64, 2, 128, 128), (128, 3, 128, 128)) and
-            not (e.startswith("f") or e.strip() == "4"))
-
-
-def train_split_active():
-    """Mirrors policy_train_split_supported() && train_split_enabled() in
-    csrc/policy_split_kernels.hip: the 64-bin 2-D and 128-bin 3-D [128,128]
-    shapes, PPO or AC, unless XH_TRAIN_KERNEL=f32."""
-    return ((B, D, H1, H2) in ((64, 2, 128, 128), (128, 3, 128, 128)) and
-            ALGO in ("ppo", "ac") and
-            not os.environ.get("XH_TRAIN_KERNEL", "").startswith("f"))
+# Which kernels ran, and the MFMA peak of their arithmetic, come from the
+# library itself (xh_trainer_kernel_info): the split train kernels run their
+# GEMMs on the bf16 matrix cores at f32 accuracy -- layer 2 six bf16 products
+# per f32 product, dW2 / dH1 three (exact 0/1 relu-mask operand), equal FLOPs,
+# so peak = dense bf16 / 4; the split rollouts' layer 2 six: dense bf16 / 6.
+# Diagnostic variables that steer kernel selection (the bench refuses them
+# unless --allow-kernel-override is given):
+KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL")
 HBM_PEAK_GBS = 8000.0
+
+
+def kernel_roofline(k, flops_per_launch, avg_ms):
+    """Roofline of one kernel from what the library says ran (an entry of
+    xh_trainer_kernel_info): its name, arithmetic and that arithmetic's MFMA
+    peak.  Nothing here re-derives the kernel selection."""
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    return {"kernel": k["kernel"], "bound": "mfma", "math": k["math"],
+            "bf16_products_per_f32_product": k["bf16_products_per_f32_product"],
+            "math_source": "xh_trainer_kernel_info",
+            "achieved": round(achieved, 2), "peak": round(k["peak_tflops"], 1),
+            "unit": "TFLOP/s", "frac": round(achieved / k["peak_tflops"], 4),
+            "frac_of_f32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4)}
 
 
 def policy_fwd_flops_per_env_step():
@@ -213,10 +205,18 @@ def main():
                     help="T, env steps per env per iteration (default: the "
                          "config's; SURVEY 8(d)'s larger-T throughput point)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--allow-kernel-override", action="store_true",
+                    help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL are "
+                         "set (A/B measurements; the line records them)")
     ap.add_argument("--reference-lr", action="store_true",
                     help="raw lr on row sums as the reference (diverges at "
                          "this batch size; default: lr_scale_rows)")
     args = ap.parse_args()
+    set_over = {k: os.environ[k] for k in KERNEL_OVERRIDES if k in os.environ}
+    if set_over and not args.allow_kernel_override:
+        print("bench.py: kernel-selection override(s) set %s; unset them or "
+              "pass --allow-kernel-override" % set_over, file=sys.stderr)
+        sys.exit(2)
     cfg = select_config(args.config)
     if args.rollout_steps:
         global T
@@ -290,18 +290,20 @@ def main():
     # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
     avg_ms = ms_pt / max(n_pt, 1)
-    split = train_split_active()
+    # what ran, and the peak of its arithmetic: from the library
+    kinfo = tr.kernel_info()
+    kt, kr = kinfo["policy_train"], kinfo["rollout_step"]
+    split = kt["math"] == "bf16_split"
     # the split kernels have one shape each: their summaries are keyed by
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
-    split_name = ("policy_train_split128" if B == 128 else "policy_train_split_kernel")
-    traffic, traffic_src, pmc = (pmc_traffic(split_name, any_shape=True)
+    traffic, traffic_src, pmc = (pmc_traffic(kt["kernel"], any_shape=True)
                                  if split else pmc_traffic())
-    train_peak = TRAIN_SPLIT_PEAK_TFLOPS if split else FP32_PEAK_TFLOPS
+    train_peak = kt["peak_tflops"]
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
     alg_bytes = n * T * (B * D + 4 + 12) + 256 * policy_param_count(D, H1, H2) * 4
-    achieved = flops_epoch / (avg_ms * 1e-3) / 1e12
+    roofline = kernel_roofline(kt, flops_epoch, avg_ms)
     # whole-iteration HBM roofline (BASELINE metric: "fraction of the HBM
     # roofline"): compulsory bytes per env-step, SURVEY §8d -- env state
     # read + write (2*B*D int8) and one trajectory record (B*D state + D item
@@ -320,7 +322,7 @@ def main():
     # peak (bf16-split at 64 bins), the value net at the f32 MFMA peak, the k
     # train epochs at the train kernel's peak; frac = that time x the
     # measured env-steps/s
-    roll_peak = SPLIT_PEAK_TFLOPS if rollout_split_active() else FP32_PEAK_TFLOPS
+    roll_peak = kr["peak_tflops"]
     it_ideal_s = (policy_fwd_flops_per_env_step() / (roll_peak * 1e12) +
                   5 * value_fwd_flops_per_row() / (FP32_PEAK_TFLOPS * 1e12) +
                   3 * EPOCHS * policy_fwd_flops_per_env_step() / (train_peak * 1e12))
@@ -351,23 +353,14 @@ def main():
                    "envs_per_gpu": n, "bins": B, "dims": D, "T": T,
                    "epochs": EPOCHS, "parallelism": "dp%d" % world,
                    "lr_scale_rows": not args.reference_lr},
-        "roofline": {"kernel": "policy_train", "bound": "mfma",
-                     "math": ("f32 operands split exactly into 3 bf16 parts, "
-                              "f32 accumulate: layer 2 6 bf16 MFMA products per "
-                              "f32 product, dW2 / dH1 3 (exact 0/1 relu-mask "
-                              "operand); peak = dense bf16 peak / 4"
-                              if split else "f32 MFMA (v_mfma_f32_32x32x2_f32)"),
-                     "achieved": round(achieved, 2), "peak": round(train_peak, 1),
-                     "unit": "TFLOP/s",
-                     "frac": round(achieved / train_peak, 4),
-                     "frac_of_f32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
+        "roofline": dict(roofline, **{
                      "traffic": traffic,
                      "traffic_source": traffic_src,
                      "mfma_busy_frac": pmc and pmc.get("mfma_busy_frac"),
                      "clock_ghz_profiled": pmc and pmc.get("clock_ghz"),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
-                     "flops_per_launch": flops_epoch},
+                     "flops_per_launch": flops_epoch}),
         "iteration_roofline": {"flops_per_env_step": it_flops,
                                "achieved": round(it_tflops, 2),
                                "unit": "TFLOP/s",
@@ -378,6 +371,7 @@ def main():
                          "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                          "frac": round(hbm_gbs / (HBM_PEAK_GBS * world), 6)},
         "health": health,
+        "kernels": kinfo,
         "runtime": runtime_info(),
         "phase_ms_per_step": {
             "rollout": round(ms_ro / args.steps, 3),

@@ -94,6 +94,8 @@ def _load():
         "xh_trainer_kernel_time": (i, [vp, C.c_char_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_long)]),
         "xh_trainer_reset_timing": (i, [vp]),
+        "xh_trainer_kernel_info": (i, [vp, C.c_char_p, sz]),
+        "xh_ctx_inject_fault": (i, [vp, i]),
         "xh_trainer_get_env_state": (i, [vp, i, i, vp, vp]),
         "xh_trainer_set_env_state": (i, [vp, i, i, vp, vp]),
         "xh_venv_create": (i, [vp, i, i, i, C.c_uint32, i, i, i,

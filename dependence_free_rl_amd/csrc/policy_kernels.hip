@@ -2283,8 +2283,11 @@ int policy_train_grid(int B, int D, int H1, int H2, int kl) {
 }
 
 hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
-                               hipStream_t s) {
+                               hipStream_t s, KernelInfo *info) {
   const int B = a.env.B, D = a.env.D;
+  KernelInfo dummy;
+  if (!info) info = &dummy;
+  info->math = kMathF32Mfma;
 #define X(XB, XD, XH1, XH2)                                                  \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
     using S = PShape<XB, XD, XH1, XH2>;                                      \
@@ -2313,6 +2316,8 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         constexpr int kRW = kRollWavesS128;                                  \
         const int wg = (a.b.N + kRW - 1) / kRW;                              \
         const int wgr = cu_count();                                          \
+        info->name = "rollout_split128_kernel";                              \
+        info->math = kMathSplitRollout;                                      \
         hipLaunchKernelGGL(rollout_split128_kernel<S>,                       \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            RollSplitLds<S>::bytes, s, a);                    \
@@ -2331,6 +2336,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         constexpr int kRW = kRollWaves128;                                   \
         const int wg = (a.b.N + kRW - 1) / kRW;                              \
         const int wgr = kRW == 8 ? grid : cu_count();                        \
+        info->name = "rollout_wave128_kernel";                               \
         hipLaunchKernelGGL(rollout_wave128_kernel<S>,                        \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            rollout_lds<S>(), s, a);                          \
@@ -2349,6 +2355,8 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         constexpr int kRW = kRollWaves64;                                    \
         const int wg = (ng + kRW - 1) / kRW;                                 \
         const int wgr = kRW == 8 ? grid : cu_count();                        \
+        info->name = "rollout_split_kernel";                                 \
+        info->math = kMathSplitRollout;                                      \
         hipLaunchKernelGGL(rollout_split_kernel<S>,                          \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            RollSplitLds<S>::bytes, s, a);                       \
@@ -2367,12 +2375,14 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         constexpr int kRW = kRollWaves64;                                    \
         const int wg = (ng + kRW - 1) / kRW;                                 \
         const int wgr = kRW == 8 ? grid : cu_count();                        \
+        info->name = "rollout_wave_kernel";                                  \
         hipLaunchKernelGGL(rollout_wave_kernel<S>,                           \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            rollout_lds<S>(), s, a);                          \
         return hipGetLastError();                                            \
       }                                                                      \
     }                                                                        \
+    info->name = S::HG == 1 ? "rollout_step_kernel" : "rollout_step128_kernel";\
     if constexpr (S::HG == 1)                                                \
       hipLaunchKernelGGL(rollout_step_kernel<S>, dim3(grid < ng ? grid : ng),\
                          dim3(256), rollout_lds<S>(), s, a);                 \
@@ -2415,10 +2425,13 @@ hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
 }
 
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
-                               int grid, hipStream_t s) {
+                               int grid, hipStream_t s, KernelInfo *info) {
   const int B = a.env.B, D = a.env.D;
+  KernelInfo dummy;
+  if (!info) info = &dummy;
+  info->math = kMathF32Mfma;
   if (policy_train_split_supported(a, H1, H2) && train_split_enabled())
-    return launch_policy_train_split(a, grid, s);
+    return launch_policy_train_split(a, grid, s, info);
 #define X(XB, XD, XH1, XH2)                                                  \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
     using S = PShape<XB, XD, XH1, XH2>;                                      \
@@ -2439,6 +2452,7 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
       attr = true;                                                           \
     }                                                                        \
     if (a.algo == kKLPPO) {                                                  \
+      info->name = "policy_train_kernel<kl>";                                \
       if constexpr (S::HG == 1)                                              \
         hipLaunchKernelGGL((policy_train_kernel<S, true>), dim3(grid),       \
                            dim3(256), train_lds<S>(), s, a);                 \
@@ -2446,6 +2460,8 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
         return hipErrorInvalidValue;                                         \
       return hipGetLastError();                                              \
     }                                                                        \
+    info->name = (S::NIT == 4 && S::NOT == 4 && (!XH_TRAIN4 || S::HG > 1))   \
+                     ? "policy_train8_kernel" : "policy_train_kernel";       \
     if constexpr (S::NIT == 4 && S::NOT == 4 && (!XH_TRAIN4 || S::HG > 1))  \
       hipLaunchKernelGGL(policy_train8_kernel<S>, dim3(grid), dim3(512),     \
                          train_lds<S>(), s, a);                              \

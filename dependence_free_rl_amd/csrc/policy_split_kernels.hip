@@ -38,6 +38,7 @@
 // images that the prologue builds in the LDS the row images use afterwards;
 // the lo parts stay in LDS images (W2' lo in the mask region's spare parts).
 #include <cstdlib>
+#include <cstring>
 
 #include "xh_device.h"
 #include "xh_kernels.h"
@@ -531,10 +532,17 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 }  // namespace split
 
 // XH_TRAIN_KERNEL=f32 keeps the f32-MFMA train kernel where the split one
-// would run (A/B measurements and the f32-vs-split tests); read per launch.
+// would run (A/B measurements and the f32-vs-split tests); =split4w keeps
+// this file's 4-wave kernel where the 8-wave one (policy_split8w_kernels.hip)
+// would run.  Diagnostic overrides, read per launch and reported by
+// xh_trainer_kernel_info.
 bool train_split_enabled() {
   const char *e = std::getenv("XH_TRAIN_KERNEL");
   return !(e && e[0] == 'f');
+}
+static bool train_split4w() {
+  const char *e = std::getenv("XH_TRAIN_KERNEL");
+  return e && std::strcmp(e, "split4w") == 0;
 }
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
@@ -545,8 +553,17 @@ bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
 }
 
 hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
-                                     hipStream_t s) {
-  if (a.env.B == kSplit128Bins) return launch_policy_train_split128(a, grid, s);
+                                     hipStream_t s, KernelInfo *info) {
+  if (info) info->math = kMathSplitTrain;
+  if (a.env.B == kSplit128Bins) {
+    if (info) info->name = "policy_train_split128_kernel";
+    return launch_policy_train_split128(a, grid, s);
+  }
+  if (!train_split4w()) {
+    if (info) info->name = "policy_train_split8w_kernel";
+    return launch_policy_train_split8w(a, grid, s);
+  }
+  if (info) info->name = "policy_train_split_kernel";
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)split::policy_train_split_kernel,

@@ -88,7 +88,12 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
                                             : ((1ull << S::LPE) - 1ull) << seg0;
   const bool over = (__ballot(neg_any) & segmask) != 0;
   const bool chosen_over = (__ballot(neg_chosen) & segmask) != 0;
-  if (!live) return;
+  if (!live) {
+    // an env not applied (masked out, or its action refused) reports no game
+    // over for this call: DONE holds this call's verdicts only
+    if (in_range && li == 0 && a.done) a.done[env] = 0;
+    return;
+  }
   uint32_t x = a.rng[env];
   if (a.mode == 1) x = mstd_mulmod(x, a.skip_mul);  // the policy's draws
   const bool reset = a.mode == 1 && over;

@@ -281,10 +281,23 @@ hipError_t launch_kl_reduce(const double *kl_part, int nparts, const int *n_end,
                             double *kl_sum, hipStream_t s);
 hipError_t launch_kl_beta_update(const double *kl_sum, float *beta,
                                  float d_targ, float *log, hipStream_t s);
+// What a launch entry point ran, recorded by the trainer for
+// xh_trainer_kernel_info: the kernel's name and its arithmetic.
+enum Math {
+  kMathF32Mfma = 0,       // f32-input MFMA (v_mfma_f32_32x32x2_f32) / f32 VALU
+  kMathSplitTrain = 1,    // bf16 MFMA on 3-part splits: layer 2 six products per
+                          // f32 product, dW2 / dH1 three (rank-1 backward)
+  kMathSplitRollout = 2   // bf16 MFMA on 3-part splits: six products (layer 2)
+};
+struct KernelInfo {
+  const char *name = nullptr;
+  int math = kMathF32Mfma;
+};
 hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
-                               hipStream_t s);
+                               hipStream_t s, KernelInfo *info = nullptr);
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
-                               int grid, hipStream_t s);
+                               int grid, hipStream_t s,
+                               KernelInfo *info = nullptr);
 // The f32-accurate bf16-split train kernels for the 64-bin 2-D
 // (policy_split_kernels.hip) and 128-bin 3-D (policy_split128_kernels.hip)
 // [128,128] shapes; XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.
@@ -292,9 +305,11 @@ constexpr int kSplit128Bins = 128, kSplit128Dims = 3;
 bool train_split_enabled();
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2);
 hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
-                                     hipStream_t s);
+                                     hipStream_t s, KernelInfo *info);
 hipError_t launch_policy_train_split128(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
+hipError_t launch_policy_train_split8w(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
                               hipStream_t s);

@@ -92,6 +92,7 @@ struct xh_ctx {
   ncclComm_t comm = nullptr;
   int trainers = 0;      // live trainers on this context
   bool closing = false;  // xh_ctx_destroy called while trainers were alive
+  int fault = 0;         // xh_ctx_inject_fault (test hook): pending fault
 };
 
 namespace {
@@ -168,6 +169,13 @@ struct xh_trainer {
   // env (B*D bin bytes then D item bytes), applied after the forget() shift
   std::map<int, std::vector<int8_t>> env_override;
   bool use_forced = false;
+  // Slots of `items` whose every env holds an item-table entry.  The train
+  // kernels fold the item's layer-1 contribution into per-table-entry biases,
+  // so learn() refuses a batch that reads a slot with any other item
+  // (xh_trainer_set_buffer accepts them for rollout-only use).
+  std::vector<char> items_ok;
+  // what the last rollout step / policy epoch launched (xh_trainer_kernel_info)
+  xh::KernelInfo last_rollout, last_train;
   bool timing = false;
   bool counted = false;  // holds a reference on ctx
   std::vector<timed_event> events;
@@ -276,24 +284,40 @@ int timed(xh_trainer *t, const char *name, F &&launch) {
   return XH_OK;
 }
 
-int allreduce(xh_trainer *t, float *buf, int n) {
+// SUM all-reduce of a flat device buffer on the trainer's stream.  An RCCL
+// failure is reported as XH_ERR_RCCL with ncclGetErrorString (and the
+// communicator's async error, if it holds one), not as a HIP error.
+int allreduce_t(xh_trainer *t, void *buf, int n, ncclDataType_t dt) {
   if (!t->ctx->comm) return XH_OK;
   hipStream_t s = t->ctx->stream;
-  return timed(t, "allreduce", [&]() -> hipError_t {
-    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum,
-                                   t->ctx->comm, s);
-    return r == ncclSuccess ? hipSuccess : hipErrorUnknown;
+  ncclResult_t r = ncclSuccess;
+  if (t->ctx->fault == XH_FAULT_RCCL_ARG) {
+    // test hook: the next all-reduce passes RCCL an invalid datatype, so RCCL
+    // itself rejects the call
+    dt = (ncclDataType_t)ncclNumTypes;
+    t->ctx->fault = 0;
+  }
+  const int st = timed(t, "allreduce", [&]() -> hipError_t {
+    r = ncclAllReduce(buf, buf, (size_t)n, dt, ncclSum, t->ctx->comm, s);
+    return hipSuccess;
   });
+  if (st != XH_OK) return st;
+  if (r != ncclSuccess) {
+    ncclResult_t ar = ncclSuccess;
+    (void)ncclCommGetAsyncError(t->ctx->comm, &ar);
+    return fail(XH_ERR_RCCL, "ncclAllReduce(%d x %s, rank %d of %d): %s%s%s", n,
+                dt == ncclFloat64 ? "f64" : dt == ncclFloat32 ? "f32" : "?",
+                t->ctx->rank, t->ctx->world,
+                ncclGetErrorString(r), ar != ncclSuccess ? "; async: " : "",
+                ar != ncclSuccess ? ncclGetErrorString(ar) : "");
+  }
+  return XH_OK;
 }
-
+int allreduce(xh_trainer *t, float *buf, int n) {
+  return allreduce_t(t, buf, n, ncclFloat32);
+}
 int allreduce_d(xh_trainer *t, double *buf, int n) {
-  if (!t->ctx->comm) return XH_OK;
-  hipStream_t s = t->ctx->stream;
-  return timed(t, "allreduce", [&]() -> hipError_t {
-    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum,
-                                   t->ctx->comm, s);
-    return r == ncclSuccess ? hipSuccess : hipErrorUnknown;
-  });
+  return allreduce_t(t, buf, n, ncclFloat64);
 }
 
 size_t buffer_bytes(const xh_trainer *t, int which) {
@@ -541,12 +565,27 @@ int apply_env_overrides(xh_trainer *t) {
   if (t->env_override.empty()) return XH_OK;
   hipStream_t s = t->ctx->stream;
   const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
-  for (auto &kv : t->env_override) {
-    const size_t e = (size_t)kv.first;
-    HIPCHK(copy_to_device(t->bins + e * BD, kv.second.data(), BD, s));
-    int8_t it[4] = {0, 0, 0, 0};
-    for (size_t d = 0; d < D; ++d) it[d] = kv.second[BD + d];
-    HIPCHK(copy_to_device(t->items + e * 4, it, 4, s));
+  // runs of consecutive env ids (the map is ordered): one bins copy and one
+  // items copy per run, a single stream synchronisation at the end
+  std::vector<int8_t> rb, ri;
+  auto it = t->env_override.begin();
+  while (it != t->env_override.end()) {
+    const size_t first = (size_t)it->first;
+    rb.clear();
+    ri.clear();
+    size_t next = first;
+    for (; it != t->env_override.end() && (size_t)it->first == next; ++it, ++next) {
+      rb.insert(rb.end(), it->second.begin(), it->second.begin() + BD);
+      int8_t item[4] = {0, 0, 0, 0};
+      for (size_t d = 0; d < D; ++d) item[d] = it->second[BD + d];
+      ri.insert(ri.end(), item, item + 4);
+    }
+    HIPCHK(hipMemcpyAsync(t->bins + first * BD, rb.data(), rb.size(),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(t->items + first * 4, ri.data(), ri.size(),
+                          hipMemcpyHostToDevice, s));
+    // pageable sources: the copies must complete before rb / ri are reused
+    HIPCHK(hipStreamSynchronize(s));
   }
   t->env_override.clear();
   return XH_OK;
@@ -556,14 +595,19 @@ int do_rollout(xh_trainer *t) {
   if (t->cfg.algo == XH_PG) return do_pg_rollout(t);
   hipStream_t s = t->ctx->stream;
   const size_t N = t->N(), T = t->T();
+  if (t->items_ok.size() != T + 1) {  // constructed envs in slot 0 only
+    t->items_ok.assign(T + 1, 0);
+    t->items_ok[0] = 1;
+  }
   if (t->need_shift) {  // replay_buffer::forget(): open trajectories continue
     HIPCHK(hipMemcpyAsync(t->bins, t->bins + T * N * t->BD(), N * t->BD(),
                           hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(t->items, t->items + T * N * 4, N * 4,
                           hipMemcpyDeviceToDevice, s));
     t->need_shift = false;
+    t->items_ok[0] = t->items_ok[T];
   }
-  CHK(apply_env_overrides(t));
+  CHK(apply_env_overrides(t));  // whole item-table entries only
   xh::RolloutArgs a{};
   a.env = t->env;
   a.b = t->batch();
@@ -578,8 +622,9 @@ int do_rollout(xh_trainer *t) {
     a.probs_out = last ? t->probs : nullptr;
     CHK(timed(t, "rollout_step", [&]() {
       return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
-                                     t->rgrid, s);
+                                     t->rgrid, s, &t->last_rollout);
     }));
+    t->items_ok[step + 1] = 1;  // items drawn from the table (get_item)
   }
   return XH_OK;
 }
@@ -620,6 +665,14 @@ xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
 
 int do_learn(xh_trainer *t) {
   if (t->cfg.algo == XH_PG) return do_pg_learn(t);
+  // the train kernels fold the item into per-table-entry biases: every slot
+  // they read must hold item-table entries only
+  for (size_t sl = 0; sl < t->T(); ++sl)
+    if (sl >= t->items_ok.size() || !t->items_ok[sl])
+      return fail(XH_ERR_STATE,
+                  "learn: slot %zu of the batch holds an item that is not an "
+                  "item-table entry (set by xh_trainer_set_buffer, or no "
+                  "rollout yet)", sl);
   hipStream_t s = t->ctx->stream;
   const xh_config &c = t->cfg;
   xh::ValueArgs va = t->vargs();
@@ -731,7 +784,7 @@ int do_learn(xh_trainer *t) {
     float *g = t->pgrads + (size_t)e * t->np;
     CHK(timed(t, "policy_train", [&]() {
       return xh::launch_policy_train(pa, c.policy_h1, c.policy_h2, t->pslab_n,
-                                     s);
+                                     s, &t->last_train);
     }));
     if (pa.trace) {
       std::vector<long long> tr(trace_n + 2 + 4096);
@@ -1093,6 +1146,39 @@ int do_pg_learn(xh_trainer *t) {
 }  // namespace
 
 // ================================================================= C ABI ==
+namespace {
+constexpr double kBf16DensePeakTflops = 2500.0;  // MI355X_MICROARCH.md
+constexpr double kF32MfmaPeakTflops = 157.3;
+
+std::string kernel_json(const xh::KernelInfo &k) {
+  char buf[256];
+  if (!k.name) return "{\"kernel\": null}";
+  const int prod = k.math == xh::kMathSplitTrain     ? 4
+                   : k.math == xh::kMathSplitRollout ? 6
+                                                     : 0;
+  if (prod)
+    std::snprintf(buf, sizeof buf,
+                  "{\"kernel\": \"%s\", \"math\": \"bf16_split\", "
+                  "\"bf16_products_per_f32_product\": %d, \"peak_tflops\": %.6g}",
+                  k.name, prod, kBf16DensePeakTflops / prod);
+  else
+    std::snprintf(buf, sizeof buf,
+                  "{\"kernel\": \"%s\", \"math\": \"f32_mfma\", "
+                  "\"bf16_products_per_f32_product\": null, \"peak_tflops\": %.6g}",
+                  k.name, kF32MfmaPeakTflops);
+  return buf;
+}
+
+std::string env_json(const char *name) {
+  const char *v = std::getenv(name);
+  if (!v) return std::string("\"") + name + "\": null";
+  std::string out = std::string("\"") + name + "\": \"";
+  for (const char *p = v; *p; ++p)
+    if (*p != '"' && *p != '\\' && (unsigned char)*p >= 32) out += *p;
+  return out + "\"";
+}
+}  // namespace
+
 extern "C" {
 
 const char *xh_last_error(void) { return g_err.c_str(); }
@@ -1594,10 +1680,39 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
         if (a[i] < 0 || a[i] >= t->cfg.bins)
           return fail(XH_ERR_INVALID, "action %d out of range", a[i]);
     }
+    const bool states = t->cfg.algo != XH_PG &&
+                        (which == XH_BUF_BINS || which == XH_BUF_ITEMS);
+    if (states && which == XH_BUF_BINS) {  // as xh_trainer_set_env_state
+      const int8_t *b = static_cast<const int8_t *>(host);
+      for (size_t i = 0; i < bytes; ++i)
+        if (b[i] < -kBinCapacity || b[i] > kBinCapacity)
+          return fail(XH_ERR_INVALID, "bin value %d outside [-%d, %d]", b[i],
+                      kBinCapacity, kBinCapacity);
+    }
+    std::vector<char> ok;
+    if (states && which == XH_BUF_ITEMS) {
+      const int8_t *v = static_cast<const int8_t *>(host);
+      const size_t N = t->N(), D = (size_t)t->cfg.dims;
+      ok.assign(t->T() + 1, 1);
+      for (size_t sl = 0; sl <= t->T(); ++sl)
+        for (size_t e = 0; e < N; ++e) {
+          const int8_t *it = v + (sl * N + e) * 4;
+          bool is_a = true, is_b = true;
+          for (size_t d = 0; d < D; ++d) {
+            if (it[d] < 0 || it[d] > kBinCapacity)
+              return fail(XH_ERR_INVALID, "item value %d outside [0, %d]", it[d],
+                          kBinCapacity);
+            is_a &= it[d] == t->env.item_a[d];
+            is_b &= it[d] == t->env.item_b[d];
+          }
+          if (!is_a && !is_b) ok[sl] = 0;
+        }
+    }
     HIPCHK(hipSetDevice(t->ctx->device));
     HIPCHK(copy_to_device(buffer_ptr(t, which), host, bytes, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     if (which == XH_BUF_BINS || which == XH_BUF_ITEMS) t->need_shift = false;
+    if (!ok.empty()) t->items_ok = std::move(ok);
     return XH_OK;
   });
 }
@@ -1697,6 +1812,33 @@ int xh_trainer_reset_timing(xh_trainer *t) {
   });
 }
 
+
+int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap) {
+  return guard([&]() -> int {
+    if (!t || !buf || cap == 0) return fail(XH_ERR_INVALID, "null arg");
+    const std::string js = "{\"rollout_step\": " + kernel_json(t->last_rollout) +
+                           ", \"policy_train\": " + kernel_json(t->last_train) +
+                           ", \"overrides\": {" + env_json("XH_TRAIN_KERNEL") +
+                           ", " + env_json("XH_ROLLOUT_KERNEL") + "}}";
+    if (js.size() + 1 > cap)
+      return fail(XH_ERR_INVALID, "kernel_info: %zu bytes needed", js.size() + 1);
+    std::memcpy(buf, js.c_str(), js.size() + 1);
+    return XH_OK;
+  });
+}
+
+int xh_ctx_inject_fault(xh_ctx *c, int kind) {
+  return guard([&]() -> int {
+    if (!c) return fail(XH_ERR_INVALID, "null ctx");
+    if (kind != XH_FAULT_NONE && kind != XH_FAULT_RCCL_ARG)
+      return fail(XH_ERR_INVALID, "unknown fault %d", kind);
+    if (kind == XH_FAULT_RCCL_ARG && !c->comm)
+      return fail(XH_ERR_STATE, "inject_fault: the context has no communicator");
+    c->fault = kind;
+    return XH_OK;
+  });
+}
+
 int xh_trainer_kernel_time(xh_trainer *t, const char *name, double *ms,
                            long *launches) {
   return guard([&]() -> int {
@@ -1761,9 +1903,13 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
       return fail(XH_ERR_INVALID, "envs [%d, %d) of %d", first, first + count,
                   t->cfg.num_envs);
     const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
+    // negative values are the overflowed (game-over) states an apply by hand
+    // leaves (bin_packing.h:53-63); an item is at most the capacity, so a bin
+    // is never below -capacity
     for (size_t i = 0; i < (size_t)count * BD; ++i)
-      if (bins[i] > kBinCapacity)
-        return fail(XH_ERR_INVALID, "bin value %d above capacity", bins[i]);
+      if (bins[i] < -kBinCapacity || bins[i] > kBinCapacity)
+        return fail(XH_ERR_INVALID, "bin value %d outside [-%d, %d]", bins[i],
+                    kBinCapacity, kBinCapacity);
     // a whole item-table entry (the train kernels carry the item columns of
     // dW1 as per-entry sums)
     for (int e = 0; e < count; ++e) {
@@ -1993,8 +2139,9 @@ int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes) {
     if (which == XH_VENV_BINS) {
       const int8_t *b = static_cast<const int8_t *>(host);
       for (size_t i = 0; i < bytes; ++i)
-        if (b[i] > kBinCapacity)
-          return fail(XH_ERR_INVALID, "venv: bin value %d above capacity", b[i]);
+        if (b[i] < -kBinCapacity || b[i] > kBinCapacity)
+          return fail(XH_ERR_INVALID, "venv: bin value %d outside [-%d, %d]",
+                      b[i], kBinCapacity, kBinCapacity);
     }
     HIPCHK(hipSetDevice(v->ctx->device));
     HIPCHK(copy_to_device(v->buf[which], host, bytes, v->ctx->stream));

@@ -58,6 +58,11 @@ class Context:
         check(_lib.lib.xh_ctx_allreduce_host(self.h, _ptr(a), a.size))
         return a
 
+    def inject_fault(self, kind=1):
+        """Test hook (xh_ctx_inject_fault): kind 1 makes the next gradient
+        all-reduce pass RCCL an invalid argument; 0 clears it."""
+        check(_lib.lib.xh_ctx_inject_fault(self.h, kind))
+
     def close(self):
         if self.h:
             check(_lib.lib.xh_ctx_destroy(self.h))
@@ -376,6 +381,15 @@ class Trainer:
         check(_lib.lib.xh_trainer_kernel_time(self.h, name.encode(), C.byref(ms),
                                               C.byref(n)))
         return ms.value, n.value
+
+    def kernel_info(self):
+        """The kernels the last rollout step / policy epoch launched and their
+        arithmetic (xh_trainer_kernel_info): {"rollout_step": {...},
+        "policy_train": {...}, "overrides": {...}}."""
+        import json
+        buf = C.create_string_buffer(2048)
+        check(_lib.lib.xh_trainer_kernel_info(self.h, buf, len(buf)))
+        return json.loads(buf.value.decode())
 
     def close(self):
         if self.h:

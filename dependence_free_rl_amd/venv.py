@@ -72,7 +72,7 @@ class VecEnv:
 
     def apply(self, mask=None):
         """environment::apply(actions[e], e) for the masked envs (no reset);
-        returns game_over per env."""
+        returns game_over per env ([N] uint8; 0 for the envs not applied)."""
         if mask is not None:
             self.set(VENV_MASK, np.asarray(mask, np.uint8))
         check(_lib.lib.xh_venv_apply(self.h, 0 if mask is None else 1))

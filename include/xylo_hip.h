@@ -63,6 +63,12 @@ int xh_ctx_destroy(xh_ctx *ctx);
 int xh_ctx_synchronize(xh_ctx *ctx);
 /* Sum-all-reduce of n floats of host memory over the job (tests/tools). */
 int xh_ctx_allreduce_host(xh_ctx *ctx, float *data, size_t n);
+/* Test hook: make the next gradient all-reduce of a trainer on this context
+ * pass RCCL an invalid argument (XH_FAULT_RCCL_ARG), so that the error path
+ * (XH_ERR_RCCL with ncclGetErrorString) runs against the real library.
+ * XH_FAULT_NONE clears it.  XH_ERR_STATE without a communicator. */
+enum { XH_FAULT_NONE = 0, XH_FAULT_RCCL_ARG = 1 };
+int xh_ctx_inject_fault(xh_ctx *ctx, int kind);
 
 /* ------------------------------------------------------------ trainer --- */
 /* XH_KLPPO: kl_ppo_learner (policy_gradient.h:310-335, ppo2_training.cc):
@@ -305,7 +311,8 @@ int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes);
  * write_obs != 0 also writes OBS of the resulting states. */
 int xh_venv_step(xh_venv *v, int write_obs);
 /* environment::apply(ACTIONS[e], e) for the envs selected by MASK (all if
- * use_mask == 0), no reset; DONE[e] = game_over after the apply. */
+ * use_mask == 0), no reset; DONE[e] = game_over after the apply, 0 for the
+ * envs this call did not apply (masked out, or an out-of-range action). */
 int xh_venv_apply(xh_venv *v, int use_mask);
 /* environment::reset(e) for the envs selected by MASK (all if use_mask == 0). */
 int xh_venv_reset(xh_venv *v, int use_mask);
@@ -346,6 +353,19 @@ int xh_trainer_set_timing(xh_trainer *t, int on);
 int xh_trainer_kernel_time(xh_trainer *t, const char *name, double *ms,
                            long *launches);
 int xh_trainer_reset_timing(xh_trainer *t);
+/* Which kernels the trainer's last rollout step and last policy epoch
+ * launched, and their arithmetic, as a JSON object written NUL-terminated
+ * into buf[cap]:
+ *   {"rollout_step": K, "policy_train": K, "overrides": {...}}
+ *   K = {"kernel": name | null (not launched yet), "math": "f32_mfma" |
+ *        "bf16_split", "bf16_products_per_f32_product": p (split kernels:
+ *        4 for the train epoch = 6 in layer 2 and 3 in dW2 / dH1, equal
+ *        FLOPs; 6 for the rollout's layer 2), "peak_tflops": the MFMA peak of
+ *        that arithmetic on MI355X (dense bf16 2500 / p, or f32 157.3)}
+ * "overrides" lists the diagnostic environment variables that steer kernel
+ * selection (XH_TRAIN_KERNEL, XH_ROLLOUT_KERNEL) with their values, or null
+ * when unset. */
+int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap);
 
 #ifdef __cplusplus
 }

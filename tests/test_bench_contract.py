@@ -51,3 +51,33 @@ def test_pmc_traffic_only_for_the_same_shape(bench):
     t5, _, _ = bench.pmc_traffic()
     # never the 64-bin kernel's counters for the 128-bin shape
     assert t5 is None or t5 != t
+
+
+def test_roofline_math_comes_from_the_library(bench):
+    """The train kernel's name, arithmetic and peak in the bench line are
+    what xh_trainer_kernel_info reported; bench.py does not re-derive the
+    kernel selection."""
+    k = {"kernel": "policy_train_split_kernel", "math": "bf16_split",
+         "bf16_products_per_f32_product": 4, "peak_tflops": 625.0}
+    r = bench.kernel_roofline(k, 857e9, 2.0)
+    assert r["kernel"] == k["kernel"] and r["math"] == "bf16_split"
+    assert r["math_source"] == "xh_trainer_kernel_info" and r["peak"] == 625.0
+    assert abs(r["achieved"] - 428.5) < 1e-6 and abs(r["frac"] - 0.6856) < 1e-4
+    k2 = dict(k, math="f32_mfma", bf16_products_per_f32_product=None,
+              peak_tflops=157.3)
+    assert bench.kernel_roofline(k2, 857e9, 2.0)["peak"] == 157.3
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert "kernel_info()" in src and "train_split_active" not in src
+
+
+@pytest.mark.parametrize("var", ["XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL"])
+def test_bench_refuses_kernel_overrides(var):
+    """A kernel-selection override in the environment stops the bench before
+    it touches the device, unless --allow-kernel-override is given."""
+    import subprocess
+    env = dict(os.environ, **{var: "f32"})
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"),
+                          "--steps", "1", "--warmup", "0"],
+                         capture_output=True, text=True, env=env, timeout=60)
+    assert out.returncode == 2 and var in out.stderr, (out.returncode, out.stderr)
+    assert out.stdout.strip() == ""

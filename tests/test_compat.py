@@ -59,3 +59,22 @@ def test_random_agent_matches_reference():
     want = golden("random_s5")["round_avg"]
     assert [k for k, _ in got] == [0, 1, 2], text[-500:]
     assert [x for _, x in got] == [fmt6(float(w)) for w in want]
+
+
+def test_save_parameters_round_trip_cpu(tmp_path):
+    """xylo::save_parameters -> raw float32 file -> mmap<float> +
+    model::set_parameters (deep_agent.cc's loader) is the identity, bit for
+    bit (no device involved)."""
+    import subprocess
+    from compat_helpers import app
+    from conftest import golden
+    if not os.path.exists(app("save_weights")):
+        pytest.skip("build/compat/save_weights not built (make compat)")
+    w = golden("deep_w20")["params"].astype("float32")
+    src = tmp_path / "w.in"
+    w.tofile(src)
+    out = subprocess.run([app("save_weights"), "copy", str(src),
+                          str(tmp_path / "w.out")], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.split() == ["equal", str(w.size)]
+    assert (tmp_path / "w.out").read_bytes() == src.read_bytes()

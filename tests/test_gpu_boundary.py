@@ -1,0 +1,131 @@
+"""Boundary checks of the C ABI that need a device: input validation of the
+state setters and the kernel report (xh_trainer_kernel_info)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(ctx, B=64, D=2, N=64, T=4, widths=(128, 128)):
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=widths,
+                 rng_state=11)
+    tr.set_params(POLICY, init_policy(D, *widths, seed=1))
+    tr.set_params(VALUE, init_value(B, D, seed=2))
+    return tr
+
+
+def test_learn_refuses_items_outside_the_item_table(ctx):
+    """The train kernels fold the item's layer-1 contribution into
+    per-item-table-entry biases, so a batch slot holding any other item is
+    refused by learn() (XH_ERR_STATE) instead of being trained as item_b;
+    rollouts from such a slot still run, and a rollout's own items (drawn from
+    the table) make the later slots valid again."""
+    from dependence_free_rl_amd import XhError
+    from dependence_free_rl_amd.trainer import BUF_ITEMS
+    tr = _trainer(ctx)
+    tr.rollout()
+    tr.learn()
+    items = tr.buffer(BUF_ITEMS).copy()
+    items[0, 5, :2] = (3, 3)  # not {4,2} / {1,2}
+    tr.set_buffer(BUF_ITEMS, items)
+    with pytest.raises(XhError, match="item-table entry"):
+        tr.learn()
+    items[0, 5, :2] = (4, 2)
+    tr.set_buffer(BUF_ITEMS, items)
+    tr.learn()
+    with pytest.raises(XhError):  # item values outside [0, capacity]
+        items[1, 0, 0] = -1
+        tr.set_buffer(BUF_ITEMS, items)
+    tr.close()
+
+
+def test_state_setters_reject_out_of_range_bins(ctx):
+    """Bin values outside [-capacity, capacity] are refused by
+    set_env_state, set_buffer(BINS) and the venv's BINS.  Negative values
+    down to -capacity stay legal: they are the overflowed (game-over) states
+    an apply by hand leaves (bin_packing.h:53-63), which the drop-in layer
+    uploads (tests/compat/bound_env_by_hand.cc)."""
+    from dependence_free_rl_amd import VecEnv, XhError
+    from dependence_free_rl_amd.trainer import BUF_BINS
+    tr = _trainer(ctx)
+    bins, items = tr.env_state(0, 2)
+    bad = bins.copy()
+    bad[1, 3, 0] = -9
+    with pytest.raises(XhError, match="outside"):
+        tr.set_env_state(0, bad, items)
+    bad[1, 3, 0] = -3  # an overflowed bin: accepted
+    tr.set_env_state(0, bad, items)
+    b = tr.buffer(BUF_BINS).copy()
+    b[0, 0, 0, 1] = 9
+    with pytest.raises(XhError, match="outside"):
+        tr.set_buffer(BUF_BINS, b)
+    tr.close()
+    env = VecEnv(ctx, num_envs=8, bins=8, dims=2, rng_state=1)
+    vb, _ = env.view()
+    vb[2, 1, 1] = -100
+    with pytest.raises(XhError, match="outside"):
+        env.set(3, vb)  # VENV_BINS
+    env.close()
+
+
+def test_env_overrides_of_many_envs(ctx):
+    """xh_trainer_set_env_state for every env (one run of consecutive envs)
+    and for scattered envs: the next rollout starts from exactly those
+    states."""
+    from dependence_free_rl_amd.trainer import BUF_BINS, BUF_ITEMS
+    N = 256
+    tr = _trainer(ctx, N=N)
+    tr.rollout()
+    tr.learn()
+    bins, items = tr.env_state(0, N)
+    rng = np.random.default_rng(0)
+    nb = rng.integers(0, 9, size=bins.shape).astype(np.int8)
+    ni = np.where(rng.random(N)[:, None] < 0.5, [[4, 2]], [[1, 2]]).astype(np.int8)
+    tr.set_env_state(0, nb, ni)
+    # scattered overrides on top: envs 3, 4, 5 and 200
+    for e in (3, 4, 5, 200):
+        nb[e] = 8 - nb[e]
+        tr.set_env_state(e, nb[e:e + 1], ni[e:e + 1])
+    tr.rollout()
+    np.testing.assert_array_equal(tr.buffer(BUF_BINS)[0], nb)
+    np.testing.assert_array_equal(tr.buffer(BUF_ITEMS)[0, :, :2], ni)
+    tr.close()
+
+
+@pytest.mark.parametrize("B,D,widths,train,roll,prod", [
+    (64, 2, (128, 128), "policy_train_split_kernel", "rollout_split_kernel", 4),
+    (8, 2, (128, 64), None, None, None),
+])
+def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
+                                    prod):
+    """xh_trainer_kernel_info reports the kernels the last rollout step and
+    policy epoch launched, their arithmetic and its MFMA peak; an override
+    variable shows up in the report and changes what runs."""
+    tr = _trainer(ctx, B=B, D=D, widths=widths)
+    k = tr.kernel_info()
+    assert k["policy_train"]["kernel"] is None  # nothing launched yet
+    tr.rollout()
+    tr.learn()
+    k = tr.kernel_info()
+    kt, kr = k["policy_train"], k["rollout_step"]
+    if train:
+        assert kt["kernel"] == train and kr["kernel"] == roll
+        assert kt["math"] == "bf16_split" and kt["bf16_products_per_f32_product"] == prod
+        assert kt["peak_tflops"] == 2500.0 / prod
+        assert kr["peak_tflops"] == pytest.approx(2500.0 / 6)
+    else:
+        assert kt["math"] == "f32_mfma" and kt["peak_tflops"] == 157.3
+        assert kt["kernel"].startswith("policy_train")
+    assert k["overrides"] == {"XH_TRAIN_KERNEL": None, "XH_ROLLOUT_KERNEL": None}
+    tr.close()
+    if train:
+        monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
+        tr = _trainer(ctx, B=B, D=D, widths=widths)
+        tr.rollout()
+        tr.learn()
+        k = tr.kernel_info()
+        assert k["overrides"]["XH_TRAIN_KERNEL"] == "f32"
+        assert k["policy_train"]["math"] == "f32_mfma"
+        assert k["policy_train"]["kernel"] == "policy_train8_kernel"
+        tr.close()

@@ -155,3 +155,80 @@ def test_bound_env_by_hand_matches_reference():
             assert np.abs(a - b).max() <= 1e-4, (got, ref)
         else:
             assert got == ref, (got, ref)
+
+
+@pytest.mark.skipif(not os.path.exists(app("save_weights")),
+                    reason="build/compat/save_weights not built (make compat)")
+def test_saved_weights_reload_and_reproduce_deep_agent(tmp_path):
+    """xylo::save_parameters round trip (f4): weights.20 set into deep_agent's
+    network, saved, and mapped back through the reference's own load path
+    (mmap<float> + model::set_parameters) comes back bit for bit; the
+    UNMODIFIED deep_agent driver run on the saved file reproduces the
+    reference's first round (fixture deep_w20_main), and the device argmax
+    evaluation of the saved-then-loaded policy gives the reference's 1000-
+    episode total, 26600 (apps/bin_packing/deep_agent.cc:21-41)."""
+    import subprocess
+    from dependence_free_rl_amd import Context, Trainer
+    from dependence_free_rl_amd.trainer import POLICY
+    g = golden("deep_w20")
+    src = tmp_path / "weights.in"
+    g["params"].astype(np.float32).tofile(src)
+    run = tmp_path / "run"
+    run.mkdir()
+    out = subprocess.run([app("save_weights"), "copy", str(src),
+                          str(run / "weights.20")], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.split() == ["equal", "8961"], out
+    saved = np.fromfile(run / "weights.20", np.float32)
+    np.testing.assert_array_equal(saved, g["params"].astype(np.float32))
+    if os.path.exists(app("deep_agent")):
+        got, text = read_rounds([app("deep_agent")], 1,
+                                dict(os.environ, XYLO_SEED="1"), cwd=str(run),
+                                timeout=300)
+        want = golden("deep_w20_main")["total_reward"][0] / 10000
+        assert got and got[0] == (0, fmt6(want)), (got, text[-1000:])
+    ctx = Context(device=0)
+    try:
+        tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1,
+                     widths=(128, 64))
+        tr.set_params(POLICY, saved)
+        r = tr.evaluate(8, 1000, int(g["x0"][0]))
+        assert r["totals"][0] == float(g["total_reward"][0]) == 26600.0
+        tr.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.skipif(not os.path.exists(app("save_weights")),
+                    reason="build/compat/save_weights not built (make compat)")
+def test_save_parameters_of_a_device_trained_policy(tmp_path):
+    """save_parameters after device training writes the trained parameters
+    (pulled from the device), in the flat model::parameters() layout the
+    device trainer and deep_agent's loader both read."""
+    import subprocess
+    from dependence_free_rl_amd import Context, Trainer, policy_param_count
+    from dependence_free_rl_amd.trainer import POLICY
+    path = tmp_path / "weights.trained"
+    out = subprocess.run([app("save_weights"), "train", str(path)],
+                         capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, XYLO_SEED="5"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    tag, n, s = out.stdout.split()
+    p = np.fromfile(path, np.float32)
+    assert tag == "params" and int(n) == p.size == policy_param_count(2, 128, 64)
+    acc = 0.0
+    for v in p.astype(np.float64).tolist():  # the program's summation order
+        acc += v
+    assert float(s) == acc
+    assert np.isfinite(p).all() and np.abs(p).max() > 0
+    ctx = Context(device=0)
+    try:
+        tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=8, steps=1,
+                     widths=(128, 64))
+        tr.set_params(POLICY, p)
+        np.testing.assert_array_equal(tr.params(POLICY), p)
+        r = tr.evaluate(8, 10, 1)
+        assert (r["steps"] > 0).all()
+        tr.close()
+    finally:
+        ctx.close()

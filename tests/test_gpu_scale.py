@@ -3,7 +3,7 @@ size-independent properties at the full BASELINE config-3 size."""
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_grad_close
+from conftest import assert_close, assert_grad_close, assert_grad_units
 
 pytestmark = pytest.mark.gpu
 
@@ -25,8 +25,12 @@ def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     ("ppo", 64, 2, (128, 128), 32, 4),   # BASELINE config 3 shape
     ("ppo", 64, 2, (128, 128), 160, 4),  # 640 groups: multi-group train blocks
     ("ppo", 32, 1, (64, 64), 64, 4),     # config 2 shape
+    # config 2 shape, 1536 two-env groups: 3 per train workgroup (2 x 256)
+    ("ppo", 32, 1, (64, 64), 768, 4),
     ("ac", 16, 2, (64, 64), 64, 8),
     ("ac", 128, 3, (128, 128), 8, 8),    # config 5 shape
+    # config 5 shape, 768 row groups: 3 per train workgroup (256)
+    ("ac", 128, 3, (128, 128), 96, 8),
     ("klppo", 64, 2, (128, 128), 16, 4),  # KL-PPO at the config-3 shape
 ])
 def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
@@ -46,6 +50,9 @@ def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
     for it in range(2):
         tr.rollout()
         acts = tr.buffer(BUF_ACTION)            # [T][N]
+        if it > 0:  # learn() from the device trainer's own parameters
+            orc.set_params(0, tr.params(POLICY))
+            orc.set_params(1, tr.params(VALUE))
         orc.rollout()                           # free-running oracle sampler
         o_choice = orc.buf(po.BUF_STEP_CHOICE).reshape(N, T).T
         np.testing.assert_array_equal(acts, o_choice)
@@ -76,6 +83,12 @@ def test_gpu_vs_oracle(ctx, algo, B, D, widths, N, T):
                           orc.buf(po.BUF_POLICY_GRADS),
                           orc.buf(po.BUF_POLICY_GRADS_MAG),
                           n_terms=len(env) * B, what="policy_grads")
+        # the tight check against the oracle's double sums (conftest)
+        assert_grad_units(tr.buffer(BUF_POLICY_GRADS).ravel(),
+                          orc.buf(po.BUF_POLICY_GRADS),
+                          orc.buf(po.BUF_POLICY_GRADS_MAG),
+                          what="vs_oracle %s B%d D%d N%d T%d it%d" % (
+                              algo, B, D, N, T, it))
         assert_close(tr.params(POLICY), orc.params(0), what="policy params")
 
 
@@ -340,9 +353,10 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T):
     ref = orc.buf(po.BUF_POLICY_GRADS)
     mag = orc.buf(po.BUF_POLICY_GRADS_MAG)
     ratios = {}
-    for kernel in ("f32", "split"):
-        if kernel == "f32":
-            monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
+    kernels = ("f32", "split4w", "split") if B == 64 else ("f32", "split")
+    for kernel in kernels:
+        if kernel in ("f32", "split4w"):
+            monkeypatch.setenv("XH_TRAIN_KERNEL", kernel)
         else:
             monkeypatch.delenv("XH_TRAIN_KERNEL", raising=False)
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
@@ -357,8 +371,9 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T):
         units = np.abs(g - ref) / np.maximum(mag * 2.0 ** -24, 1e-30)
         ratios[kernel] = (float(units.max()), float(np.median(units[mag > 0])))
     print("policy-gradient error in u * sum|terms| (max, median):", ratios)
-    assert ratios["split"][0] <= 3 * ratios["f32"][0] + 8, ratios
-    assert ratios["split"][1] <= 3 * ratios["f32"][1] + 1, ratios
+    for k in kernels[1:]:
+        assert ratios[k][0] <= 3 * ratios["f32"][0] + 8, ratios
+        assert ratios[k][1] <= 3 * ratios["f32"][1] + 1, ratios
 
 
 @pytest.mark.parametrize("algo,N,B,D,T", [("ppo", 32768, 64, 2, 4),

@@ -13,47 +13,63 @@ iteration) and leaves the result bit-identical."""
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_grad_close
+from conftest import assert_close, assert_grad_close, assert_grad_units
 
 pytestmark = pytest.mark.gpu
 
 
 
-@pytest.mark.parametrize("n", [64, 16384])
-def test_two_shards_sum_to_full_batch(ctx, n):
+@pytest.mark.parametrize("B,D,widths,n", [
+    (8, 2, (128, 64), 64),
+    (8, 2, (128, 64), 16384),
+    # the headline shape on its own kernels (bf16-split rollout and train):
+    # a config-4 rank's situation (env_offset != 0, num_envs_global > N)
+    (64, 2, (128, 128), 128),     # oracle-pinned, several groups per workgroup
+    (64, 2, (128, 128), 16384),   # config 3 = two config-4 ranks' shards
+])
+def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_ADV, BUF_BINS,
-                                                BUF_POLD, BUF_POLICY_GRADS,
+                                                BUF_ITEMS, BUF_POLD,
+                                                BUF_POLICY_GRADS, BUF_RNG,
                                                 BUF_VALUE_GRAD)
-    B, D, T = 8, 2, 4
-    pp, vp = init_policy(D, 128, 64, seed=21), init_value(B, D, seed=22)
+    T = 4
+    pp, vp = init_policy(D, *widths, seed=21), init_value(B, D, seed=22)
 
     def make(num, off):
         tr = Trainer(ctx, bins=B, dims=D, num_envs=num, steps=T,
-                     widths=(128, 64), lr_policy=0.0, lr_value=0.0,
+                     widths=widths, lr_policy=0.0, lr_value=0.0,
                      rng_state=31337, num_envs_global=2 * n, env_offset=off)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         return tr
 
     full, s0, s1 = make(2 * n, 0), make(n, 0), make(n, n)
+    if B == 64:  # the headline kernels ran, on every trainer
+        for tr in (full, s0, s1):
+            tr.rollout()
+            tr.learn()
+            k = tr.kernel_info()
+            assert k["policy_train"]["kernel"] == "policy_train_split_kernel", k
+            assert k["rollout_step"]["kernel"] == "rollout_split_kernel", k
+        full, s0, s1 = make(2 * n, 0), make(n, 0), make(n, n)
     orc = None
-    if n <= 64:  # the oracle's sum|terms| per entry states the fp32 bound
+    if n <= 128:  # the oracle's sum|terms| per entry states the fp32 bound
         from oracle import pyoracle as po
         orc = po.Trainer(po.OR_PPO, B, D, 2 * n, T,
-                         po.perbin_model(2 * D, [128, 64], po.OR_SOFTMAX), pp,
+                         po.perbin_model(2 * D, list(widths), po.OR_SOFTMAX), pp,
                          po.full_model(B * 2 * D, [64, 32], 1), vp,
                          lr_pi=0.0, lr_v=0.0, x0=31337)
     for it in range(2):
         for tr in (full, s0, s1):
             tr.rollout()
-        for buf in (BUF_ACTION, BUF_POLD):
+        for buf in (BUF_ACTION, BUF_POLD, BUF_BINS, BUF_ITEMS):
             f = full.buffer(buf)
             np.testing.assert_array_equal(f[:, :n], s0.buffer(buf))
             np.testing.assert_array_equal(f[:, n:], s1.buffer(buf))
-        f = full.buffer(BUF_BINS)
-        np.testing.assert_array_equal(f[:, :n], s0.buffer(BUF_BINS))
-        np.testing.assert_array_equal(f[:, n:], s1.buffer(BUF_BINS))
+        r = full.buffer(BUF_RNG)
+        np.testing.assert_array_equal(r[:n], s0.buffer(BUF_RNG))
+        np.testing.assert_array_equal(r[n:], s1.buffer(BUF_RNG))
         for tr in (full, s0, s1):
             tr.learn()
         if orc is not None:
@@ -67,15 +83,29 @@ def test_two_shards_sum_to_full_batch(ctx, n):
         g = s0.buffer(BUF_POLICY_GRADS)[0] + s1.buffer(BUF_POLICY_GRADS)[0]
         f = full.buffer(BUF_POLICY_GRADS)[0]
         if orc is not None:
-            # two fp32 evaluation orders of the same sums (sides = 2)
+            # two fp32 evaluation orders of the same sums (sides = 2), and
+            # each against the oracle's double sums (the tight budget)
             mag = orc.buf(po.BUF_POLICY_GRADS_MAG)[:g.size]
+            ref = orc.buf(po.BUF_POLICY_GRADS)[:g.size]
             rows = len(orc.buf(po.BUF_ROW_ENV))
             assert_grad_close(g, f, mag, n_terms=rows * B, sides=2,
                               what="policy grad sum")
-        else:  # fp32 sums over 131k env-steps in different orders
+            tag = "shards B%d n%d it%d" % (B, n, it)
+            assert_grad_units(f, ref, mag, what=tag + " full")
+            assert_grad_units(g, ref, mag, what=tag + " shard sum")
+        else:
+            # fp32 sums over 2n * T * B rows in different orders, no oracle
+            # at this size: a sanity bound (the oracle-pinned check of the
+            # same kernels is the n = 128 case).  Policy-gradient entries
+            # cancel to ~1e-3 of their sum |terms| (conftest), so at 8.4 M
+            # rows two summation orders differ by ~1e-4 of |g| (measured
+            # 2.9e-4 relative L2 at 64 bins, 2e-6 at 8 bins)
             rel = np.linalg.norm(g - f) / np.linalg.norm(f)
             worst = np.abs(g - f).max() / np.abs(f).max()
-            assert rel <= 1e-5 and worst <= 1e-4, (rel, worst)
+            lim = (1e-5, 1e-4) if B == 8 else (2e-3, 4e-3)
+            print("shards B%d n%d it%d: rel L2 %.3g, worst %.3g" % (B, n, it, rel,
+                                                                  worst))
+            assert rel <= lim[0] and worst <= lim[1], (rel, worst)
 
 
 def test_rccl_one_rank_communicator(ctx):
@@ -102,5 +132,36 @@ def test_rccl_one_rank_communicator(ctx):
         np.testing.assert_array_equal(v0, v1)
         x = np.arange(7, dtype=np.float32)
         np.testing.assert_array_equal(rc.allreduce_host(x), x)
+    finally:
+        rc.close()
+
+
+def test_rccl_error_is_reported_as_rccl(ctx):
+    """A failing ncclAllReduce surfaces as XH_ERR_RCCL with RCCL's own message
+    (xh_ctx_inject_fault makes the next gradient all-reduce pass RCCL an
+    invalid datatype, so the library itself rejects the call), and the
+    trainer keeps working after it."""
+    from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer, XhError,
+                                        init_policy, init_value)
+    from dependence_free_rl_amd._lib import XH_ERR_RCCL
+    with pytest.raises(XhError, match="status %d" % 4):  # no communicator
+        ctx.inject_fault(1)
+    rc = Context(device=0, rank=0, world=1, uid=Context.unique_id())
+    try:
+        tr = Trainer(rc, bins=8, dims=2, num_envs=64, steps=4, widths=(128, 64),
+                     rng_state=5)
+        tr.set_params(POLICY, init_policy(2, 128, 64, seed=1))
+        tr.set_params(VALUE, init_value(8, 2, seed=2))
+        tr.rollout()
+        rc.inject_fault(1)
+        with pytest.raises(XhError) as ei:
+            tr.learn()
+        msg = str(ei.value)
+        assert ("status %d" % XH_ERR_RCCL) in msg and "ncclAllReduce" in msg, msg
+        print(msg)
+        tr.rollout()  # the fault was one-shot: the next iteration runs
+        tr.learn()
+        assert np.isfinite(tr.params(POLICY)).all()
+        tr.close()
     finally:
         rc.close()

@@ -146,6 +146,7 @@ def test_venv_apply_reset_masks(ctx, B, D):
         acts = rng.integers(0, B, N).astype(np.int32)
         env.set_actions(acts)
         done = env.apply(mask)
+        assert (done[mask == 0] == 0).all()  # only this call's verdicts
         for e in np.nonzero(mask)[0]:
             x = po.C.c_uint32(int(xs[e]))
             po.lib().or_env_apply(po.C.byref(cfg), po._ptr(st[e][0]),
