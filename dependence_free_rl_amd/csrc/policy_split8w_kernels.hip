@@ -39,6 +39,29 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Phase stamps (trace build: this file and policy_kernels.hip compiled with
+// -DXH_DIAG_TRACE=1, run with XH_PHASE_TRACE=1): lane 0 of every wave of the
+// first kTraceBlocks workgroups records the cycle counter at these phase
+// boundaries of its first kTraceGroups groups: 0 group start, 1 layer 2 +
+// logits done, 2 after barrier 1, 3 softmax / masks / g (x) H1 done, 4 dW2
+// done, 5 after its barrier, 6 dH1 / dW1 done, 7 layer 1 (next) done.
+#ifndef XH_DIAG_TRACE
+#define XH_DIAG_TRACE 0
+#endif
+#if XH_DIAG_TRACE
+#define S8_STAMP(a, gi, w, lane, slot)                                          \
+  do {                                                                        \
+    if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups &&      \
+        (lane) == 0)                                                          \
+      (a).trace[((blockIdx.x * kTraceGroups + (gi)) * 8 + (w)) * kTraceSlots + \
+                (slot)] = clock64();                                          \
+  } while (0)
+#else
+#define S8_STAMP(a, gi, w, lane, slot) \
+  do {                                 \
+  } while (0)
+#endif
+
 namespace xh {
 namespace s8w {
 
@@ -283,8 +306,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8w_kernel(
   if ((int)blockIdx.x < ngroups) layer1(0, stb0, fo0);
   __syncthreads();
 
-  int par = 0;
-  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  int par = 0, gi = 0;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x, ++gi) {
+    S8_STAMP(a, gi, w, l, 0);
     const int gn = g + gridDim.x;
     const bool has_next = gn < ngroups;
     // opaque copies of the per-lane LDS bases and of the f32 vector offset:
@@ -346,7 +370,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8w_kernel(
         if (G == 0) lf[F_Z + (16 * rt + li) * 8 + w] = zp;
       }
     }
+    S8_STAMP(a, gi, w, l, 1);
     __syncthreads();
+    S8_STAMP(a, gi, w, l, 2);
 
     // ---- softmax -> loss gradient g (lane = row = bin, every wave) ->
     // dW3 / db2 sums, the mask image, g (x) H1 over the H1 image; wave 0
@@ -409,6 +435,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8w_kernel(
         st_split(img, stb + 4096 * rt, t);
       }
     }
+    S8_STAMP(a, gi, w, l, 3);
     __syncthreads();
 
     // ---- dW2[:, tile w] += M^T (g (x) H1): K = the 64 rows (two K-steps);
@@ -429,7 +456,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8w_kernel(
         }
       }
     }
+    S8_STAMP(a, gi, w, l, 4);
     __syncthreads();  // g (x) H1 consumed: the next group's layer 1 may write
+    S8_STAMP(a, gi, w, l, 5);
     // ---- dH1[rows 16 rt + 4G + j][i = 16w + li] = M . W2' -> relu' -> dW1 /
     // db1 / item sums, r-tile by r-tile; layer 1 of the next group in the
     // same phase
@@ -472,7 +501,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8w_kernel(
       else
         sb += sg;
     }
+    S8_STAMP(a, gi, w, l, 6);
     if (has_next) layer1(par ^ 1, stb, fo);
+    S8_STAMP(a, gi, w, l, 7);
     par ^= 1;
     __syncthreads();  // mask / g (x) H1 consumed; the next images written
   }

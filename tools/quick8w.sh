@@ -8,3 +8,5 @@ for k in split4w default; do
   timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline $A > gpurun_out/q8w_bench_$k.json 2> gpurun_out/q8w_bench_$k.err || { cat gpurun_out/q8w_bench_$k.err | tail; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/q8w_bench_$k.json'));print('$k', d['value'], d['roofline']['kernel'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['phase_ms_per_step'])"
 done
+XH_LIB_PATH=build/t8/libxylo_hip.so XH_PHASE_TRACE=1 timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/t8.json 2> gpurun_out/t8.err || { tail -5 gpurun_out/t8.err; exit 1; }
+grep "phase trace" gpurun_out/t8.err | tail -1
