@@ -532,17 +532,18 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 }  // namespace split
 
 // XH_TRAIN_KERNEL=f32 keeps the f32-MFMA train kernel where the split one
-// would run (A/B measurements and the f32-vs-split tests); =split4w keeps
-// this file's 4-wave kernel where the 8-wave one (policy_split8w_kernels.hip)
-// would run.  Diagnostic overrides, read per launch and reported by
+// would run (A/B measurements and the f32-vs-split tests); for the 64-bin
+// shape =split8w keeps the unpipelined 8-wave kernel
+// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel where
+// the pipelined one (policy_split8wp_kernels.hip) would run.  Diagnostic overrides, read per launch and reported by
 // xh_trainer_kernel_info.
 bool train_split_enabled() {
   const char *e = std::getenv("XH_TRAIN_KERNEL");
   return !(e && e[0] == 'f');
 }
-static bool train_split4w() {
+static bool train_kernel_is(const char *name) {
   const char *e = std::getenv("XH_TRAIN_KERNEL");
-  return e && std::strcmp(e, "split4w") == 0;
+  return e && std::strcmp(e, name) == 0;
 }
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
@@ -559,9 +560,13 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
     if (info) info->name = "policy_train_split128_kernel";
     return launch_policy_train_split128(a, grid, s);
   }
-  if (!train_split4w()) {
+  if (train_kernel_is("split8w")) {
     if (info) info->name = "policy_train_split8w_kernel";
     return launch_policy_train_split8w(a, grid, s);
+  }
+  if (!train_kernel_is("split4w")) {
+    if (info) info->name = "policy_train_split8wp_kernel";
+    return launch_policy_train_split8wp(a, grid, s);
   }
   if (info) info->name = "policy_train_split_kernel";
   static bool attr = false;

@@ -3,6 +3,8 @@ state setters and the kernel report (xh_trainer_kernel_info)."""
 import numpy as np
 import pytest
 
+from conftest import HEADLINE_TRAIN_KERNEL
+
 pytestmark = pytest.mark.gpu
 
 
@@ -94,7 +96,7 @@ def test_env_overrides_of_many_envs(ctx):
 
 
 @pytest.mark.parametrize("B,D,widths,train,roll,prod", [
-    (64, 2, (128, 128), "policy_train_split_kernel", "rollout_split_kernel", 4),
+    (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 4),
     (8, 2, (128, 64), None, None, None),
 ])
 def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,

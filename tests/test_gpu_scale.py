@@ -353,9 +353,9 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T):
     ref = orc.buf(po.BUF_POLICY_GRADS)
     mag = orc.buf(po.BUF_POLICY_GRADS_MAG)
     ratios = {}
-    kernels = ("f32", "split4w", "split") if B == 64 else ("f32", "split")
+    kernels = ("f32", "split4w", "split8w", "split") if B == 64 else ("f32", "split")
     for kernel in kernels:
-        if kernel in ("f32", "split4w"):
+        if kernel != "split":
             monkeypatch.setenv("XH_TRAIN_KERNEL", kernel)
         else:
             monkeypatch.delenv("XH_TRAIN_KERNEL", raising=False)

@@ -13,7 +13,8 @@ iteration) and leaves the result bit-identical."""
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_grad_close, assert_grad_units
+from conftest import (HEADLINE_TRAIN_KERNEL, assert_close, assert_grad_close,
+                      assert_grad_units)
 
 pytestmark = pytest.mark.gpu
 
@@ -50,7 +51,7 @@ def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
             tr.rollout()
             tr.learn()
             k = tr.kernel_info()
-            assert k["policy_train"]["kernel"] == "policy_train_split_kernel", k
+            assert k["policy_train"]["kernel"] == HEADLINE_TRAIN_KERNEL, k
             assert k["rollout_step"]["kernel"] == "rollout_split_kernel", k
         full, s0, s1 = make(2 * n, 0), make(n, 0), make(n, n)
     orc = None
