@@ -171,9 +171,9 @@ def cpu_baseline():
 def pmc_traffic(kernel="policy_train", any_shape=False):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     FETCH_SIZE / WRITE_SIZE summary (separate --pmc passes; see
-    tools/pmc_summary.py).  Raw counters (FETCH_SIZE is not x2-corrected: the
-    kernel's reads are narrow int8 loads, for which the gfx950 x2 correction
-    of wide streaming reads does not apply)."""
+    tools/pmc_summary.py): 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read
+    correction measured for 1- to 16-byte lanes by tools/probes/fetch_probe.hip
+    (older summaries without the calibration are converted here)."""
     import glob
     # newest round first (profiles/<round><pass>[_c<config>]_pmc_summary.json);
     # only a summary of this very shape counts (PShape<B, D, H1, H2>)
@@ -188,7 +188,10 @@ def pmc_traffic(kernel="policy_train", any_shape=False):
                   if k.startswith(kernel) and (any_shape or shape in v.get("kernel", ""))
                   and "hbm_bytes" in v), None)
         if s:
-            return s["hbm_bytes"], os.path.relpath(path, REPO), s
+            hbm = s["hbm_bytes"]
+            if "hbm_bytes_raw_reads" not in s:  # pre-calibration summary
+                hbm = s["fetch_bytes_x2"] + s["write_bytes"]
+            return hbm, os.path.relpath(path, REPO), s
     return None, None, None
 
 

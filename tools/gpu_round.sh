@@ -14,7 +14,7 @@ cp $O/profiles/${TAG}_c*_pmc_summary.json profiles/
 timeout -k 10 400 python -u bench.py > $O/profiles/${TAG}_bench_config3.json.log 2>&1 || { tail -5 $O/profiles/${TAG}_bench_config3.json.log; exit 1; }
 tail -1 $O/profiles/${TAG}_bench_config3.json.log > $O/profiles/${TAG}_bench_config3.json
 for c in 2 5; do
-  timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline > $O/b$c.log 2>&1 || { tail -5 $O/b$c.log; exit 1; }
+  timeout -k 10 400 python -u bench.py --config $c > $O/b$c.log 2>&1 || { tail -5 $O/b$c.log; exit 1; }
   tail -1 $O/b$c.log > $O/profiles/${TAG}_bench_config$c.json
 done
 timeout -k 10 300 python -u bench.py --rollout-steps 32 --steps 3 --warmup 1 --no-cpu-baseline > $O/bT32.log 2>&1 || { tail -5 $O/bT32.log; exit 1; }

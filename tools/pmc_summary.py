@@ -4,10 +4,12 @@
     [PROFILE_OUT=dir] python tools/pmc_summary.py <tag> <trace_dir> <fetch_dir> <write_dir>
 
 Per kernel: average duration (kernel trace) and HBM bytes per launch from the
-separate FETCH_SIZE / WRITE_SIZE passes (units: KB; MI355X_MICROARCH.md §HBM:
-on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide 16-B/lane streaming
-loads -- both the raw and the x2-corrected read figure are recorded; other
-access widths are uncalibrated).
+separate FETCH_SIZE / WRITE_SIZE passes (units: KB).  On gfx950 FETCH_SIZE
+counts half the bytes read (MI355X_MICROARCH.md §HBM for 16-B/lane streaming
+loads; tools/probes/fetch_probe.hip measured the same 1/2 for 1-, 2-, 4- and
+16-byte lanes: 1 GiB read -> 524298 KB, profiles/r03_probe_fetch_write.txt),
+WRITE_SIZE the bytes written (256 MiB of 4-byte stores -> 262144 KB), so
+hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE; the raw read figure is kept too.
 """
 import collections
 import csv
@@ -58,7 +60,7 @@ def main(tag, trace, fetch, write, *sq_dirs):
         wb = ws.get(k, 0.0) * 1024
         summary[short(k)] = {"kernel": k, "avg_ns": dur.get(k), "fetch_bytes_raw": fb,
                       "fetch_bytes_x2": 2 * fb, "write_bytes": wb,
-                      "hbm_bytes": fb + wb, "hbm_bytes_x2_reads": 2 * fb + wb}
+                      "hbm_bytes": 2 * fb + wb, "hbm_bytes_raw_reads": fb + wb}
     # SQ / GRBM passes (MFMA utilisation): raw per-dispatch means, plus
     #   clock_ghz       = GRBM_GUI_ACTIVE / 8 XCDs / duration
     #   mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024
