@@ -83,6 +83,10 @@ HEADLINE_TRAIN_KERNEL = "policy_train_split8wp_kernel"
 
 GRAD_UNITS_MEDIAN = 1.0
 GRAD_UNITS_P99 = 100.0
+# PPO / KL-PPO epochs after the first start from parameters each side updated
+# itself (r03 klppo_b8d2: epoch-3 p99 198 units where epoch 0 holds 13), so
+# their p99 carries the drift of the earlier epochs' updates
+GRAD_UNITS_P99_DRIFT = 1000.0
 
 
 def grad_units(x, ref, mag):

@@ -10,8 +10,8 @@ values, advantages, gradients, parameters.
 import numpy as np
 import pytest
 
-from conftest import (assert_close, assert_grad_close, assert_grad_units,
-                      assert_params_close, golden, noise_mask)
+from conftest import (GRAD_UNITS_P99_DRIFT, assert_close, assert_grad_close,
+                      assert_grad_units, assert_params_close, golden, noise_mask)
 from gpu_helpers import (default_lr, meta, row_index, step_major,
                          trainer_from_golden)
 
@@ -177,12 +177,21 @@ def test_learn_matches_reference(ctx, name):
         # the two sides' noise-level entries step apart after the first
         # update (conftest.noise_mask): there only the first epoch's
         # gradient, which both compute on the same parameters.
-        k = tr.num_params(POLICY) if adam[POLICY] else None
-        if not (adam[POLICY] and it > 0):
-            assert_grad_units(tr.buffer(BUF_POLICY_GRADS).ravel()[:k],
-                              orc.buf(po.BUF_POLICY_GRADS)[:k],
-                              orc.buf(po.BUF_POLICY_GRADS_MAG)[:k],
-                              what="golden %s %spolicy_grads" % (name, p))
+        # Epoch 0 runs on identical parameters on both sides: the tight
+        # budget.  Epochs 1..k-1 start from parameters each side updated
+        # itself (f32 steps of gradients that differ by the units above), so
+        # a cancelled entry also carries that drift: the drift budget.
+        npi = tr.num_params(POLICY)
+        dev = tr.buffer(BUF_POLICY_GRADS).reshape(-1, npi)
+        ref = np.asarray(orc.buf(po.BUF_POLICY_GRADS)).reshape(-1, npi)
+        mag = np.asarray(orc.buf(po.BUF_POLICY_GRADS_MAG)).reshape(-1, npi)
+        for ep in range(1 if adam[POLICY] else dev.shape[0]):
+            if adam[POLICY] and it > 0:
+                break
+            budget = {} if ep == 0 else {"p99_units": GRAD_UNITS_P99_DRIFT}
+            assert_grad_units(dev[ep], ref[ep], mag[ep],
+                              what="golden %s %sepoch%d_policy_grads" % (name, p, ep),
+                              **budget)
         for w, what, gk in ((VALUE, "value_params", "value_grad"),
                             (POLICY, "policy_params", "policy_grads")):
             gr = g[p + gk]
