@@ -12,7 +12,7 @@ if [ "$1" = run ]; then
   mkdir -p gpurun_out
   for rep in 1 2; do
     for n in "$@"; do
-      XH_TRAIN_KERNEL=$K XH_LIB_PATH=build/ab_$n/libxylo_hip.so timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --allow-kernel-override > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { tail -3 gpurun_out/ab_$n.err; exit 1; }
+      XH_TRAIN_KERNEL=$K XH_LIB_PATH=build/ab_$n/libxylo_hip.so timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --allow-kernel-override $BENCH_ARGS > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { tail -3 gpurun_out/ab_$n.err; exit 1; }
       python -c "import json;d=json.load(open('gpurun_out/ab_$n.json'));print('$n', d['roofline']['kernel'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['value'])"
     done
   done
