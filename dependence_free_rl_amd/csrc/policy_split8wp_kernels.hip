@@ -49,6 +49,29 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Phase stamps (trace build, tools/build_trace8wp.sh: -DXH_DIAG_TRACE=1, run
+// with XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
+// workgroups records the cycle counter at 0 X start, 1 layer 2 (+ group j's
+// VALU) done, 2 partial logits written, 3 after the X barrier, 4 dW2 / dH1
+// blocks done, 5 dW1 tail done, 6 after the Y barrier (7 = 6), for its first
+// kTraceGroups groups.
+#ifndef XH_DIAG_TRACE
+#define XH_DIAG_TRACE 0
+#endif
+#if XH_DIAG_TRACE
+#define S8P_STAMP(a, gi, w, lane, slot)                                         \
+  do {                                                                        \
+    if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups &&      \
+        (lane) == 0)                                                          \
+      (a).trace[((blockIdx.x * kTraceGroups + (gi)) * 8 + (w)) * kTraceSlots + \
+                (slot)] = clock64();                                          \
+  } while (0)
+#else
+#define S8P_STAMP(a, gi, w, lane, slot) \
+  do {                                  \
+  } while (0)
+#endif
+
 namespace xh {
 namespace s8p {
 
@@ -257,11 +280,12 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
   float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float accB3 = 0.0f, w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
 
-  // wave 0 stages group j: raw loads (two registers: the row's bins; lanes
-  // 0-3 the action, old probability, advantage and the item's first two
-  // coordinates) one group ahead of the stores into slot s (bins / 8 in row
-  // order and in the C layout's order, whether the item is item_a, the
-  // record); nothing waits for the loads until the stores
+  // wave 0 stages group j+2 during X(j): raw loads at its start (two
+  // registers: the row's bins; lanes 0-3 the action, old probability,
+  // advantage and the item's first two coordinates), the stores into slot s
+  // (bins / 8 in row order and in the C layout's order, whether the item is
+  // item_a, the record) late in the same phase, so the loads' latency hides
+  // under layer 2
   struct Raw {
     int bi, rec;
   };
@@ -271,16 +295,13 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
     asm volatile("" : "+v"(lo));
     const int bins =
         *reinterpret_cast<const unsigned short *>(a.b.bins + ti * (kB * kD) + lo);
-    int rec;  // exec-masked loads into one register
-    if (l == 0)
-      rec = a.b.action[ti];
-    else if (l == 1)
-      rec = __float_as_int(a.b.pold[ti]);
-    else if (l == 2)
-      rec = __float_as_int(a.adv[ti]);
-    else
-      rec = *reinterpret_cast<const unsigned short *>(a.b.items + ti * 4);
-    return Raw{bins, rec};
+    // one branch-free load per lane (lanes 3.. the item's first two
+    // coordinates), so nothing waits for it before its use
+    const int *src = l == 0   ? a.b.action + ti
+                     : l == 1 ? reinterpret_cast<const int *>(a.b.pold + ti)
+                     : l == 2 ? reinterpret_cast<const int *>(a.adv + ti)
+                              : reinterpret_cast<const int *>(a.b.items + ti * 4);
+    return Raw{bins, *src};
   };
   auto stage_store = [&](const Raw &r, int s) {
     const float x0 = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
@@ -355,16 +376,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
     }
   };
   // partial logits of rows 16 rt + li over this wave's features -> F_Z[zs]
+  auto partial_rt = [&](const f32x4 &pre, const f32x4 &w3, int zs, int rt) {
+    float zp = relu(pre[0]) * w3[0];
+    zp = fmaf(relu(pre[1]), w3[1], zp);
+    zp = fmaf(relu(pre[2]), w3[2], zp);
+    zp = fmaf(relu(pre[3]), w3[3], zp);
+    zp = sum_groups(zp);
+    if (G == 0) lf[F_Z + zs * 512 + (16 * rt + li) * 8 + w] = zp;
+  };
   auto partials = [&](const f32x4 (&pre)[4], const f32x4 &w3, int zs) {
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
-      float zp = relu(pre[rt][0]) * w3[0];
-      zp = fmaf(relu(pre[rt][1]), w3[1], zp);
-      zp = fmaf(relu(pre[rt][2]), w3[2], zp);
-      zp = fmaf(relu(pre[rt][3]), w3[3], zp);
-      zp = sum_groups(zp);
-      if (G == 0) lf[F_Z + zs * 512 + (16 * rt + li) * 8 + w] = zp;
-    }
+    for (int rt = 0; rt < 4; ++rt) partial_rt(pre[rt], w3, zs, rt);
   };
   auto no_task = [](int) {};
 
@@ -375,7 +397,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
   if (w == 0) {
     stage_store(stage_load(0), 0);
     stage_store(stage_load(1), 1);
-    raw = stage_load(2);
   }
   __syncthreads();
   layer1_all(0, stb0);
@@ -392,6 +413,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
         trw1 = trw10, stb = stb0;
     asm volatile("" : "+v"(rdb), "+v"(rdw), "+v"(trm0), "+v"(trm1), "+v"(trw0),
                  "+v"(trw1), "+v"(stb), "+s"(gstep));
+    S8P_STAMP(a, j, w, l, 0);
+    if (w == 0) raw = stage_load(j + 2);
     const float *xim = lf + F_X + cs * 128;
     // T-layout constants of feature 16w + li (re-read: cheaper than holding)
     const float w1a = lf[F_W1T + 16 * w + li], w1b = lf[F_W1T + kH + 16 * w + li];
@@ -484,12 +507,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
         }
       } else if (k == 24) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
-      } else if (k == 16) {
-        // wave 0: group j+2's rows into slot ns, group j+3's loaded
-        if (w == 0) {
-          stage_store(raw, ns);
-          raw = stage_load(j + 3);
-        }
+      } else if (k == 30) {
+        // wave 0: group j+2's rows (loaded at the start of X(j)) into slot ns
+        if (w == 0) stage_store(raw, ns);
       }
       if (k < 4) {
         // the relu masks of r-tile k (C layout) -> mask image
@@ -502,8 +522,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
     };
     f32x4 pre_nx[4];
     layer2(rdb, rdw, pre_nx, xtask);
+    S8P_STAMP(a, j, w, l, 1);
     partials(pre_nx, w3, (j + 1) & 1);
+    S8P_STAMP(a, j, w, l, 2);
     __syncthreads();
+    S8P_STAMP(a, j, w, l, 3);
 
     // ================= Y(j): dW2 / dH1 of group j with VALU of j, j+2 =====
     // 32 blocks of three MFMAs: b < 16 dW2 (ks = b / 8, ot = b % 8: dW2 +=
@@ -536,6 +559,21 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
         sg += d;
         w0 = fmaf(d, dx0[jj], w0);
         w1 = fmaf(d, dx1[jj], w1);
+      };
+      // layer 1 of group j+2, r-tile rt of the feature block at store base
+      // sb: half 0 the values, half 1 the split stores
+      auto layer1_rt = [&](int rt, int half, int sb) {
+        if (half == 0) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            t1[jj] = relu(fmaf(xp1[rt], wb[jj], fmaf(xp0[rt], wa[jj], bb[jj])));
+        } else {
+          bf16x4 ph, pm, pl;
+          split4(t1, ph, pm, pl);
+          st4(sb + L_H1 + 4096 * rt, ph);
+          st4(sb + L_H1 + kImg + 4096 * rt, pm);
+          st4(sb + L_H1 + 2 * kImg + 4096 * rt, pl);
+        }
       };
       auto ytask = [&](int b) {
         if (b == 0) {
@@ -578,18 +616,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
         } else if (b >= 8 && b < 16) {
           // layer 1 of group j+2, r-tile (b - 8) / 2: values, then the
           // split stores
-          const int rt = (b - 8) >> 1;
-          if ((b & 1) == 0) {
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
-              t1[jj] = relu(fmaf(xp1[rt], wb[jj], fmaf(xp0[rt], wa[jj], bb[jj])));
-          } else {
-            bf16x4 ph, pm, pl;
-            split4(t1, ph, pm, pl);
-            st4(stb + L_H1 + 4096 * rt, ph);
-            st4(stb + L_H1 + kImg + 4096 * rt, pm);
-            st4(stb + L_H1 + 2 * kImg + 4096 * rt, pl);
-          }
+          layer1_rt((b - 8) >> 1, b & 1, stb);
         } else {
           const int rt = (b - 16) >> 2, s = (b - 16) & 3;
           if (rt > 0) dw1(s, rt - 1);
@@ -627,14 +654,18 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wp_kernel(
         A_c = A_n;
         L_c = L_n;
       }
+      S8P_STAMP(a, j, w, l, 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s) dw1(s, 3);
       if (item_cur)
         sa += sg;
       else
         sb += sg;
+      S8P_STAMP(a, j, w, l, 5);
     }
     __syncthreads();
+    S8P_STAMP(a, j, w, l, 6);
+    S8P_STAMP(a, j, w, l, 7);
     // rotate the pipeline
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];

@@ -813,6 +813,28 @@ int do_learn(xh_trainer *t) {
                    " dH1 %.0f dW2 %.0f end+bar3 %.0f\n", n,
                    sum[0] / n, sum[1] / n, sum[2] / n, sum[3] / n, sum[4] / n,
                    sum[5] / n, sum[6] / n, sum[7] / n, sum[8] / n);
+      if (std::getenv("XH_PHASE_TRACE_WAVES")) {  // the same means per wave
+        for (int w = 0; w < 8; ++w) {
+          double sw[xh::kTraceSlots + 1] = {0};
+          long nw = 0;
+          for (int b = 0; b < xh::kTraceBlocks; ++b)
+            for (int gi = 1; gi + 1 < xh::kTraceGroups; ++gi) {
+              const long long *p =
+                  &tr[((b * xh::kTraceGroups + gi) * 8 + w) * xh::kTraceSlots];
+              const long long *pn = p + 8 * xh::kTraceSlots;
+              if (!p[0] || !pn[0]) continue;
+              for (int k = 1; k < xh::kTraceSlots; ++k) sw[k] += p[k] - p[k - 1];
+              sw[xh::kTraceSlots] += pn[0] - p[xh::kTraceSlots - 1];
+              sw[0] += pn[0] - p[0];
+              ++nw;
+            }
+          if (!nw) continue;
+          std::fprintf(stderr, "  wave %d:", w);
+          for (int k = 0; k <= xh::kTraceSlots; ++k)
+            std::fprintf(stderr, " %.0f", sw[k] / nw);
+          std::fprintf(stderr, "\n");
+        }
+      }
       {  // kernel-level stamps (4-wave kernel: the last trace group)
         double k1 = 0, k2 = 0, k3 = 0;
         long kn = 0;
