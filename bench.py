@@ -74,6 +74,7 @@ def kernel_roofline(k, flops_per_launch, avg_ms):
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     return {"kernel": k["kernel"], "bound": "mfma", "math": k["math"],
             "bf16_products_per_f32_product": k["bf16_products_per_f32_product"],
+            "products_per_f32_product": k.get("products_per_f32_product"),
             "math_source": "xh_trainer_kernel_info",
             "achieved": round(achieved, 2), "peak": round(k["peak_tflops"], 1),
             "unit": "TFLOP/s", "frac": round(achieved / k["peak_tflops"], 4),
@@ -296,7 +297,7 @@ def main():
     # what ran, and the peak of its arithmetic: from the library
     kinfo = tr.kernel_info()
     kt, kr = kinfo["policy_train"], kinfo["rollout_step"]
-    split = kt["math"] == "bf16_split"
+    split = kt["math"] != "f32_mfma"
     # the split kernels have one shape each: their summaries are keyed by
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
     traffic, traffic_src, pmc = (pmc_traffic(kt["kernel"], any_shape=True)

@@ -533,9 +533,12 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 
 // XH_TRAIN_KERNEL=f32 keeps the f32-MFMA train kernel where the split one
 // would run (A/B measurements and the f32-vs-split tests); for the 64-bin
-// shape =split8w keeps the unpipelined 8-wave kernel
-// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel where
-// the pipelined one (policy_split8wp_kernels.hip) would run.  Diagnostic overrides, read per launch and reported by
+// shape the default is the pipelined 8-wave kernel on f16 pairs
+// (policy_split8wh_kernels.hip); =split8wp keeps its all-bf16 form
+// (policy_split8wp_kernels.hip), =split4p the pipelined 4-wave one
+// (policy_split4p_kernels.hip), =split8w the unpipelined 8-wave one
+// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel.
+// Diagnostic overrides, read per launch and reported by
 // xh_trainer_kernel_info.
 bool train_split_enabled() {
   const char *e = std::getenv("XH_TRAIN_KERNEL");
@@ -564,9 +567,20 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
     if (info) info->name = "policy_train_split8w_kernel";
     return launch_policy_train_split8w(a, grid, s);
   }
-  if (!train_kernel_is("split4w")) {
+  if (train_kernel_is("split8wp")) {
     if (info) info->name = "policy_train_split8wp_kernel";
     return launch_policy_train_split8wp(a, grid, s);
+  }
+  if (train_kernel_is("split4p")) {
+    if (info) info->name = "policy_train_split4p_kernel";
+    return launch_policy_train_split4p(a, grid, s);
+  }
+  if (!train_kernel_is("split4w")) {
+    if (info) {
+      info->name = "policy_train_split8wh_kernel";
+      info->math = kMathSplitTrainF16;
+    }
+    return launch_policy_train_split8wh(a, grid, s);
   }
   if (info) info->name = "policy_train_split_kernel";
   static bool attr = false;

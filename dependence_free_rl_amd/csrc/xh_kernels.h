@@ -287,7 +287,9 @@ enum Math {
   kMathF32Mfma = 0,       // f32-input MFMA (v_mfma_f32_32x32x2_f32) / f32 VALU
   kMathSplitTrain = 1,    // bf16 MFMA on 3-part splits: layer 2 six products per
                           // f32 product, dW2 / dH1 three (rank-1 backward)
-  kMathSplitRollout = 2   // bf16 MFMA on 3-part splits: six products (layer 2)
+  kMathSplitRollout = 2,  // bf16 MFMA on 3-part splits: six products (layer 2)
+  kMathSplitTrainF16 = 3  // layer 2 three f16 MFMAs per f32 product (scaled f16
+                          // pairs), dH1 two, dW2 three bf16 (8 per 3 products)
 };
 struct KernelInfo {
   const char *name = nullptr;
@@ -311,6 +313,10 @@ hipError_t launch_policy_train_split128(const PolicyTrainArgs &a, int grid,
 hipError_t launch_policy_train_split8w(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8wp(const PolicyTrainArgs &a, int grid,
+                                        hipStream_t s);
+hipError_t launch_policy_train_split4p(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
+hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,

@@ -1173,20 +1173,31 @@ constexpr double kBf16DensePeakTflops = 2500.0;  // MI355X_MICROARCH.md
 constexpr double kF32MfmaPeakTflops = 157.3;
 
 std::string kernel_json(const xh::KernelInfo &k) {
-  char buf[256];
+  char buf[320];
   if (!k.name) return "{\"kernel\": null}";
-  const int prod = k.math == xh::kMathSplitTrain     ? 4
-                   : k.math == xh::kMathSplitRollout ? 6
-                                                     : 0;
-  if (prod)
+  // MFMA products per f32 product of the kernel's arithmetic (equal FLOPs
+  // per GEMM): bf16 / f16 run at the same dense rate (MI355X_MICROARCH.md)
+  const double prod = k.math == xh::kMathSplitTrain      ? 4.0
+                      : k.math == xh::kMathSplitRollout  ? 6.0
+                      : k.math == xh::kMathSplitTrainF16 ? 8.0 / 3.0
+                                                         : 0.0;
+  if (k.math == xh::kMathSplitTrainF16)
+    std::snprintf(buf, sizeof buf,
+                  "{\"kernel\": \"%s\", \"math\": \"f16_pair_bf16_split\", "
+                  "\"bf16_products_per_f32_product\": null, "
+                  "\"products_per_f32_product\": %.6g, \"peak_tflops\": %.6g}",
+                  k.name, prod, kBf16DensePeakTflops / prod);
+  else if (prod > 0)
     std::snprintf(buf, sizeof buf,
                   "{\"kernel\": \"%s\", \"math\": \"bf16_split\", "
-                  "\"bf16_products_per_f32_product\": %d, \"peak_tflops\": %.6g}",
-                  k.name, prod, kBf16DensePeakTflops / prod);
+                  "\"bf16_products_per_f32_product\": %d, "
+                  "\"products_per_f32_product\": %d, \"peak_tflops\": %.6g}",
+                  k.name, (int)prod, (int)prod, kBf16DensePeakTflops / prod);
   else
     std::snprintf(buf, sizeof buf,
                   "{\"kernel\": \"%s\", \"math\": \"f32_mfma\", "
-                  "\"bf16_products_per_f32_product\": null, \"peak_tflops\": %.6g}",
+                  "\"bf16_products_per_f32_product\": null, "
+                  "\"products_per_f32_product\": null, \"peak_tflops\": %.6g}",
                   k.name, kF32MfmaPeakTflops);
   return buf;
 }

@@ -96,7 +96,7 @@ def test_env_overrides_of_many_envs(ctx):
 
 
 @pytest.mark.parametrize("B,D,widths,train,roll,prod", [
-    (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 4),
+    (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 8.0 / 3.0),
     (8, 2, (128, 64), None, None, None),
 ])
 def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
@@ -113,8 +113,11 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
     kt, kr = k["policy_train"], k["rollout_step"]
     if train:
         assert kt["kernel"] == train and kr["kernel"] == roll
-        assert kt["math"] == "bf16_split" and kt["bf16_products_per_f32_product"] == prod
-        assert kt["peak_tflops"] == 2500.0 / prod
+        # f16 pairs in layer 2 (three products) and dH1 (two), the bf16
+        # split in dW2 (three): 8 MFMA products per 3 f32 products
+        assert kt["math"] == "f16_pair_bf16_split"
+        assert kt["products_per_f32_product"] == pytest.approx(prod, rel=1e-5)
+        assert kt["peak_tflops"] == pytest.approx(2500.0 / prod, rel=1e-5)
         assert kr["peak_tflops"] == pytest.approx(2500.0 / 6)
     else:
         assert kt["math"] == "f32_mfma" and kt["peak_tflops"] == 157.3
