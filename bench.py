@@ -57,10 +57,11 @@ def select_config(c):
     return k
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 # Which kernels ran, and the MFMA peak of their arithmetic, come from the
-# library itself (xh_trainer_kernel_info): the split train kernels run their
-# GEMMs on the bf16 matrix cores at f32 accuracy -- layer 2 six bf16 products
-# per f32 product, dW2 / dH1 three (exact 0/1 relu-mask operand), equal FLOPs,
-# so peak = dense bf16 / 4; the split rollouts' layer 2 six: dense bf16 / 6.
+# library itself (xh_trainer_kernel_info): the 64- and 128-bin train kernels
+# run layer 2 on f16 pairs (three f16 products per f32 product), dH1 on f16
+# pairs against the exact mask (two) and dW2 on the exact bf16 split (three):
+# eight products per three f32 products, peak = dense 2500 / (8/3); the
+# split rollouts' layer 2 on f16 pairs: dense 2500 / 3.
 # Diagnostic variables that steer kernel selection (the bench refuses them
 # unless --allow-kernel-override is given):
 KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL")

@@ -620,61 +620,95 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
   }
 }
 
-// ============================== rollout step, wave per env, bf16 split ==
-// The wave-per-env rollout of the 64-bin [128,128] shape with layer 2 on the
-// bf16 matrix cores at f32 accuracy (xh_split.h: six bf16 products of exact
-// three-part splits per f32 product).  Layer 1 (f32 MFMA, the same chain,
-// bias and relu as rollout_wave_kernel) leaves H1 tile `it` of an r-tile in
-// accumulator registers (lane = row, register j = feature acc_row(j, h)); its
-// registers 8s .. 8s+7, split, are directly the B operand of K-slice s of
+// ============================== rollout step, wave per env, f16 pairs ==
+// The wave-per-env rollout of the [128,128] shapes with layer 2 on the f16
+// matrix cores at f32-class accuracy (xh_split.h, f16 pairs: W2 and H1 each
+// scaled by a power of two chosen per launch -- max|W2|, and the bound
+// |H1[r][i]| <= sum_k |W1[i][k]| + |b1[i]| since every observation feature
+// is in [-1, 1] -- and split exactly into two f16 parts; three f16 products
+// per K slice).  Layer 1 (f32 MFMA, the same chain, bias and relu as
+// rollout_wave_kernel) leaves H1 tile `it` of an r-tile in accumulator
+// registers (lane = row, register j = feature acc_row(j, h)); its registers
+// 8s .. 8s+7, scaled and split, are directly the B operand of K-slice s of
 // the 32x32x16 MFMA, whose k order is then feature it*32 + 16s + 8(e>>2) +
 // 4h + (e&3) for element e of lane half h.  W2 is staged with the columns
 // of every 16-block permuted to that order (bits 2 and 3 of the column
 // swapped), so each A fragment is one ds_read_b128 of the swizzled image.
-// 2.5x fewer MFMA cycles than rollout_wave_kernel; the logits differ from
-// it in the last places (f32-class: tests/test_gpu_scale.py), the sampler,
-// the env step and everything after are the same code.
-// LDS (bytes): three W2 part images [o][permuted i] (96 KB), then f32 W1
-// [H1][F0], b1, b2, w3, b3.
+// The pre-activations stay in units of S_W S_H: b2 is staged times that and
+// w3 divided by it, so relu(pre + b2) w3 takes the same roundings as the
+// unscaled values.  The logits differ from rollout_wave_kernel's in the
+// last places (f32-class: tests/test_gpu_scale.py); the sampler, the env
+// step and everything after are the same code.
+// LDS (bytes): two W2 part images [o][permuted i] (64 KB), then f32 W1
+// [H1][F0], b1, b2 S_W S_H, w3 / (S_W S_H), b3, S_H, the scale reduction.
 template <class S>
 struct RollSplitLds {
   static constexpr int W2 = 0;
-  static constexpr int F = 3 * 128 * kImgRow;
+  static constexpr int F = 2 * 128 * kImgRow;
   static constexpr int W1 = 0, B1 = S::H1 * S::F0, B2 = B1 + S::H1, W3 = B2 + S::H2,
-                       B3 = W3 + S::H2;
-  static constexpr size_t bytes = F + sizeof(float) * (B3 + 4);
+                       B3 = W3 + S::H2, SH = B3 + 1, SC = B3 + 4;
+  static constexpr size_t bytes = F + sizeof(float) * (SC + 2 * 16);
 };
 
-// Stage the split W2 images (columns permuted, see above) and the small
-// parameters of the split rollouts.
+// Stage the f16-pair W2 images (columns permuted, see above) and the small
+// parameters of the split rollouts; every thread of the block calls it (it
+// synchronises the block).
 template <class S>
 __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
                                                     char *lds) {
   using L = RollSplitLds<S>;
   float *lf = reinterpret_cast<float *>(lds + L::F);
   const PolicyLayout PL{S::F0, S::H1, S::H2};
+  // the scales: max|W2| and the H1 bound, reduced over the block
+  float mw = 0.0f, mh = 0.0f;
+  for (int e = threadIdx.x; e < S::H2 * S::H1; e += blockDim.x)
+    mw = fmaxf(mw, fabsf(P[PL.oW2() + e]));
+  for (int i = threadIdx.x; i < S::H1; i += blockDim.x) {
+    float v = fabsf(P[PL.ob1() + i]);
+    for (int k = 0; k < S::F0; ++k) v += fabsf(P[PL.oW1() + i * S::F0 + k]);
+    mh = fmaxf(mh, v);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    mw = fmaxf(mw, __shfl_xor(mw, o, kWave));
+    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+  }
+  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    lf[L::SC + wv] = mw;
+    lf[L::SC + 16 + wv] = mh;
+  }
+  __syncthreads();
+  float MW = 0.0f, MH = 0.0f;
+  for (int v = 0; v < nw; ++v) {
+    MW = fmaxf(MW, lf[L::SC + v]);
+    MH = fmaxf(MH, lf[L::SC + 16 + v]);
+  }
+  const float SW = f16_scale_for(MW), SH = f16_scale_for(MH), S2 = SW * SH;
   for (int e = threadIdx.x; e < S::H2 * S::H1; e += blockDim.x) {
     const int o = e >> 7, i = e & 127;
     // logical column i -> its slot: bits 2 and 3 swapped within the 16-block
     const int c = (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1);
-    __bf16 x0, x1, x2;
-    split3(P[PL.oW2() + e], x0, x1, x2);
+    _Float16 x0, x1;
+    split2h(P[PL.oW2() + e] * SW, x0, x1);
     const int off = img_off(o, c >> 3) + 2 * (c & 7);
-    *reinterpret_cast<__bf16 *>(lds + L::W2 + off) = x0;
-    *reinterpret_cast<__bf16 *>(lds + L::W2 + 128 * kImgRow + off) = x1;
-    *reinterpret_cast<__bf16 *>(lds + L::W2 + 256 * kImgRow + off) = x2;
+    *reinterpret_cast<_Float16 *>(lds + L::W2 + off) = x0;
+    *reinterpret_cast<_Float16 *>(lds + L::W2 + 128 * kImgRow + off) = x1;
   }
   for (int i = threadIdx.x; i < S::H1 * S::F0; i += blockDim.x) lf[L::W1 + i] = P[PL.oW1() + i];
   for (int i = threadIdx.x; i < S::H1; i += blockDim.x) {
     lf[L::B1 + i] = P[PL.ob1() + i];
-    lf[L::B2 + i] = P[PL.ob2() + i];
-    lf[L::W3 + i] = P[PL.ow3() + i];
+    lf[L::B2 + i] = P[PL.ob2() + i] * S2;
+    lf[L::W3 + i] = P[PL.ow3() + i] * (1.0f / S2);
   }
-  if (threadIdx.x == 0) lf[L::B3] = P[PL.ob3()];
+  if (threadIdx.x == 0) {
+    lf[L::B3] = P[PL.ob3()];
+    lf[L::SH] = SH;
+  }
 }
 
 // Partial logits (without b3) of the two r-tiles of `cur` (64 rows) by the
-// split layer 2: zl[rt] = the logit sum of row rt*32 + (lane & 31).
+// f16-pair layer 2: zl[rt] = the logit sum of row rt*32 + (lane & 31).
 template <class S>
 __device__ __forceinline__ void wave_logits_split(const char *lds,
                                                   const RowRaw<S> &cur,
@@ -682,8 +716,8 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
   using L = RollSplitLds<S>;
   const float *lf = reinterpret_cast<const float *>(lds + L::F);
   const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
-  const char *w2i[3] = {lds + L::W2, lds + L::W2 + 128 * kImgRow,
-                        lds + L::W2 + 256 * kImgRow};
+  const char *w2i[2] = {lds + L::W2, lds + L::W2 + 128 * kImgRow};
+  const float SH = lf[L::SH];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     float xb[S::S1];
@@ -704,7 +738,7 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
         const float wa = k < S::F0 ? lf[L::W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
         t1 = mfma32(wa, xb[s1], t1);
       }
-      bf16x8 bfr[2][3];
+      f16x8 bfr[2][2];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
@@ -712,12 +746,11 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float v = relu(t1[4 * q + u] + bq[u]);
-          __bf16 p0, p1, p2;
-          split3(v, p0, p1, p2);
+          _Float16 p0, p1;
+          split2h(v * SH, p0, p1);
           const int j = 4 * q + u;
           bfr[j >> 3][0][j & 7] = p0;
           bfr[j >> 3][1][j & 7] = p1;
-          bfr[j >> 3][2][j & 7] = p2;
         }
       }
 #pragma unroll
@@ -725,10 +758,14 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
         const int rb = row_base(ot * 32 + lr, h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 af[3];
+          f16x8 af[2];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) af[p] = ld_row(w2i[p], rb, 2 * it + s);
-          pre[ot] = mfma_split6(af, bfr[s], pre[ot]);
+          for (int p = 0; p < 2; ++p)
+            af[p] = __builtin_bit_cast(f16x8, ld_row(w2i[p], rb, 2 * it + s));
+          // the three f16 products, small terms first
+          pre[ot] = mfma_f16(af[1], bfr[s][0], pre[ot]);
+          pre[ot] = mfma_f16(af[0], bfr[s][1], pre[ot]);
+          pre[ot] = mfma_f16(af[0], bfr[s][0], pre[ot]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }

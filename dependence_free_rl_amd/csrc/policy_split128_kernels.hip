@@ -1,8 +1,12 @@
 // policy_split128_kernels.hip -- the 128-bin 3-D train epoch (BASELINE
-// config 5) on the split GEMMs with the rank-1 backward: the math and the
-// image layout of policy_split_kernels.hip (see its header), one env of 128
-// rows per group.  A file of its own so that each kernel is compiled with
-// the flags measured best for it (Makefile).
+// config 5) with the rank-1 backward: the math and the image layout of
+// policy_split_kernels.hip (see its header), one env of 128 rows per group,
+// with layer 2 and dH1 on f16 pairs (xh_split.h: power-of-two scales chosen
+// per launch from the parameters, three f16 MFMAs per K slice for layer 2
+// instead of the bf16 split's six, two for dH1 instead of three; dW2 keeps
+// the exact three-part bf16 split of g (x) H1, whose scale is not known
+// before the kernel).  A file of its own so that each kernel is compiled
+// with the flags measured best for it (Makefile).
 #include "xh_device.h"
 #include "xh_kernels.h"
 #include "xh_split.h"
@@ -23,18 +27,22 @@ namespace s128 {
 constexpr int kB = 128, kD = 3, kF0 = 2 * kD, kH1 = 128, kH2 = 128, kS1 = 2;
 constexpr int kThreads = 256;
 constexpr int kImg = 64 * kImgRow;
-constexpr int L_H1 = 0, L_DA = 3 * kImg, L_W2 = 0;
-constexpr int L_W2LO = 6 * kImg;
-constexpr int L_F = L_W2LO + 128 * kImgRow;
+// LDS: the row images (H1 as two f16 parts, then g (x) H1 as three bf16
+// parts), the bf16 mask image (dW2's transposed reads) and its f16 copy
+// (dH1's row reads), then f32
+constexpr int L_H1 = 0, L_DA = 3 * kImg, L_MKH = 4 * kImg;
+constexpr int L_F = 5 * kImg;
 constexpr int F_W1 = 0;                  // [H1][F0]
-constexpr int F_B2 = F_W1 + kH1 * kF0;   // [H2]
+constexpr int F_B2 = F_W1 + kH1 * kF0;   // [H2] b2 S_W S_H (layer 2's C input)
 constexpr int F_W3 = F_B2 + kH2;         // [H2]
-constexpr int F_B3 = F_W3 + kH2;         // [4]
-constexpr int F_B1F = F_B3 + 4;          // [2][H1]
+constexpr int F_B3 = F_W3 + kH2;         // [4]: b3, the scales S_W, S_D, S_H
+constexpr int F_W3S = F_B3 + 4;          // [H2] w3 / (S_W S_H): the logits
+constexpr int F_B1F = F_W3S + kH2;       // [2][H1]
 constexpr int F_Z = F_B1F + 2 * kH1;     // [4][128] partial logits
 constexpr int F_X = F_Z + 4 * 128;       // [3 dims][64 rows] of the current half
 constexpr int F_G = F_X + kD * 64;       // [64] the half's row gradients
-constexpr int F_END = F_G + 64;
+constexpr int F_SC = F_G + 64;           // [16] the scales' reduction
+constexpr int F_END = F_SC + 16;
 constexpr int L_B2A = L_F + sizeof(float) * F_END;
 constexpr size_t kLds = L_B2A + 4 * 4 * 64 * 16;
 static_assert(kLds <= 160 * 1024, "LDS");
@@ -45,11 +53,11 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
   constexpr int kB = s128::kB, kD = s128::kD, kF0 = s128::kF0, kH1 = s128::kH1,
                 kH2 = s128::kH2, kS1 = s128::kS1, kThreads = s128::kThreads,
                 kImg = s128::kImg;
-  constexpr int L_H1 = s128::L_H1, L_DA = s128::L_DA, L_W2 = s128::L_W2,
-                L_W2LO = s128::L_W2LO, L_F = s128::L_F, L_B2A = s128::L_B2A;
+  constexpr int L_H1 = s128::L_H1, L_DA = s128::L_DA, L_MKH = s128::L_MKH,
+                L_F = s128::L_F, L_B2A = s128::L_B2A;
   constexpr int F_W1 = s128::F_W1, F_B2 = s128::F_B2, F_W3 = s128::F_W3,
-                F_B3 = s128::F_B3, F_B1F = s128::F_B1F, F_Z = s128::F_Z,
-                F_X = s128::F_X, F_G = s128::F_G;
+                F_B3 = s128::F_B3, F_W3S = s128::F_W3S, F_B1F = s128::F_B1F,
+                F_Z = s128::F_Z, F_X = s128::F_X, F_G = s128::F_G, F_SC = s128::F_SC;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
   const PolicyLayout PL{kF0, kH1, kH2};
@@ -58,19 +66,59 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
   const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, lr = lane & 31, h = lane >> 5;
 
-  for (int e = tid; e < kH2 * kH1; e += kThreads) {
-    const int o = e >> 7, i = e & 127;
-    __bf16 x0, x1, x2;
-    split3(P[PL.oW2() + e], x0, x1, x2);
-    const int off = img_off(o, i >> 3) + 2 * (i & 7);
-    *reinterpret_cast<__bf16 *>(lds + L_W2 + off) = x0;
-    *reinterpret_cast<__bf16 *>(lds + L_W2 + 128 * kImgRow + off) = x1;
-    *reinterpret_cast<__bf16 *>(lds + L_W2LO + off) = x2;
+  // the scales (maxima over the parameters; every workgroup the same): W2,
+  // W2' = diag(w3) W2, and H1 <= |W1[i][0..2]| + |b1_item[i]| (|bins / 8| <= 1)
+  {
+    float mw = 0.0f, md = 0.0f, mh = 0.0f;
+    for (int e = tid; e < kH2 * kH1; e += kThreads) {
+      const float v = P[PL.oW2() + e];
+      mw = fmaxf(mw, fabsf(v));
+      md = fmaxf(md, fabsf(v * P[PL.ow3() + (e >> 7)]));
+    }
+    if (tid < kH1) {
+      float ba = P[PL.ob1() + tid], bb = ba, wsum = 0.0f;
+#pragma unroll
+      for (int d = 0; d < kD; ++d) {
+        const float wv = P[PL.oW1() + tid * kF0 + kD + d];
+        ba += wv * ((float)a.env.item_a[d] / (float)kCapacity);
+        bb += wv * ((float)a.env.item_b[d] / (float)kCapacity);
+        wsum += fabsf(P[PL.oW1() + tid * kF0 + d]);
+      }
+      mh = wsum + fmaxf(fabsf(ba), fabsf(bb));
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      mw = fmaxf(mw, __shfl_xor(mw, o, kWave));
+      md = fmaxf(md, __shfl_xor(md, o, kWave));
+      mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    }
+    if (lane == 0) {
+      lf[F_SC + q] = mw;
+      lf[F_SC + 4 + q] = md;
+      lf[F_SC + 8 + q] = mh;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float MW = 0.0f, MD = 0.0f, MH = 0.0f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        MW = fmaxf(MW, lf[F_SC + v]);
+        MD = fmaxf(MD, lf[F_SC + 4 + v]);
+        MH = fmaxf(MH, lf[F_SC + 8 + v]);
+      }
+      lf[F_B3 + 1] = f16_scale_for(MW);
+      lf[F_B3 + 2] = f16_scale_for(MD);
+      lf[F_B3 + 3] = f16_scale_for(MH);
+    }
+    __syncthreads();
   }
+  const float SW = lf[F_B3 + 1], SD = lf[F_B3 + 2], SH = lf[F_B3 + 3];
+  const float S2 = SW * SH;  // layer 2's pre-activations are in units of S2
   for (int i = tid; i < kH1 * kF0; i += kThreads) lf[F_W1 + i] = P[PL.oW1() + i];
   for (int i = tid; i < kH2; i += kThreads) {
-    lf[F_B2 + i] = P[PL.ob2() + i];
+    lf[F_B2 + i] = P[PL.ob2() + i] * S2;
     lf[F_W3 + i] = P[PL.ow3() + i];
+    lf[F_W3S + i] = P[PL.ow3() + i] * (1.0f / S2);
   }
   if (tid == 0) lf[F_B3] = P[PL.ob3()];
   for (int i = tid; i < 2 * kH1; i += kThreads) {
@@ -84,7 +132,6 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
   }
   __syncthreads();
   const int rb0_ = row_base(lr, h), rb1_ = row_base(32 + lr, h);
-  const int rbw_ = row_base(q * 32 + lr, h);
   const int tb0_ = tr_base(lane, 0), tb1_ = tr_base(lane, 1);
   const int tq0_ = tb0_ ^ (64 * q), tq1_ = tb1_ ^ (64 * q);
   const int sb0 = st_base(lr, h), sb1 = st_base(32 + lr, h);
@@ -92,37 +139,27 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     asm volatile("" : "+v"(v));
     return v;
   };
-  bf16x8 wl[8][2], wd[8][2];
+  // f16-pair fragments of tile q: wl = layer 2's A operand (rows o = 32 q +
+  // lr, k = i = 16 s + 8 h + j), wd = dH1's B operand (k = o = 16 s + 8 h +
+  // j, column i = 32 q + lr), straight from the parameters
+  f16x8 wl[8][2], wd[8][2];
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const char *img = lds + L_W2 + p * 128 * kImgRow;
-      wl[s][p] = ld_row(img, rbw_, s);
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * h + j;
+      _Float16 x0, x1;
+      split2h(P[PL.oW2() + (q * 32 + lr) * kH1 + k] * SW, x0, x1);
+      wl[s][0][j] = x0;
+      wl[s][1][j] = x1;
+      split2h((P[PL.oW2() + k * kH1 + q * 32 + lr] * P[PL.ow3() + k]) * SD, x0, x1);
+      wd[s][0][j] = x0;
+      wd[s][1][j] = x1;
     }
-  __syncthreads();
-  // W2' = diag(w3) W2 for dH1 (as the 64-row kernel)
-  for (int e = tid; e < kH2 * kH1; e += kThreads) {
-    const int o = e >> 7, i = e & 127;
-    __bf16 x0, x1, x2;
-    split3(P[PL.oW2() + e] * P[PL.ow3() + o], x0, x1, x2);
-    const int off = img_off(o, i >> 3) + 2 * (i & 7);
-    *reinterpret_cast<__bf16 *>(lds + L_W2 + off) = x0;
-    *reinterpret_cast<__bf16 *>(lds + L_W2 + 128 * kImgRow + off) = x1;
-    *reinterpret_cast<__bf16 *>(lds + L_DA + kImg + off) = x2;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      wd[s][p] = ld_tr(lds + L_W2 + p * 128 * kImgRow, tq0_, tq1_, s);
-  __syncthreads();
 
   char *h1i[3] = {lds + L_H1, lds + L_H1 + kImg, lds + L_H1 + 2 * kImg};
-  char *mki = lds + L_DA;  // the 0/1 mask image M
-  const char *w2lo = lds + L_W2LO;
-  const char *w2dlo = lds + L_DA + kImg;  // W2' lo
+  char *mki = lds + L_DA;   // the 0/1 mask image M (bf16)
+  char *mkh = lds + L_MKH;  // the same as f16
   float *xim = lf + F_X;
   const int N = a.b.N, T = a.b.T;
   const int ngroups = T * N;
@@ -187,32 +224,33 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
       }
 #pragma unroll
       for (int j = 0; j < 16; ++j) t1[j] = relu(t1[j]);
-      img_store_split_b(h1i[0], h1i[1], h1i[2], rt == 0 ? sb0 : sb1, q * 32, t1);
+      img_store_h2(h1i[0], h1i[1], rt == 0 ? sb0 : sb1, q * 32, t1, SH);
     }
   };
   // ---- layer 2 of the imaged half (H2 tile q, both r-tiles)
   auto layer2 = [&](f32x16s (&pre)[2]) {
-    const int rb0 = opq(rb0_), rb1 = opq(rb1_), rbw = opq(rbw_);
+    const int rb0 = opq(rb0_), rb1 = opq(rb1_);
     pre[0] = lds_acc16(lf + F_B2, q * 32, h);
     pre[1] = pre[0];
-    bf16x8 lo_c = ld_row(w2lo, rbw, 0), lo_n = lo_c, b_c[3], b_n[3];
+    f16x8 b_c[2], b_n[2];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) b_c[p] = ld_row(h1i[p], rb0, 0);
+    for (int p = 0; p < 2; ++p) b_c[p] = __builtin_bit_cast(f16x8, ld_row(h1i[p], rb0, 0));
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       const int s = st >> 1, rt = st & 1;
       if (st + 1 < 16) {
         const int s1 = (st + 1) >> 1, r1 = (st + 1) & 1;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) b_n[p] = ld_row(h1i[p], r1 ? rb1 : rb0, s1);
-        if (r1 == 0) lo_n = ld_row(w2lo, rbw, s1);
+        for (int p = 0; p < 2; ++p)
+          b_n[p] = __builtin_bit_cast(f16x8, ld_row(h1i[p], r1 ? rb1 : rb0, s1));
       }
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 wa[3] = {wl[s][0], wl[s][1], lo_c};
-      pre[rt] = mfma_split6(wa, b_c, pre[rt]);
+      // the three f16 products, small terms first
+      pre[rt] = mfma_f16(wl[s][1], b_c[0], pre[rt]);
+      pre[rt] = mfma_f16(wl[s][0], b_c[1], pre[rt]);
+      pre[rt] = mfma_f16(wl[s][0], b_c[0], pre[rt]);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b_c[p] = b_n[p];
-      if (rt == 1) lo_c = lo_n;
+      for (int p = 0; p < 2; ++p) b_c[p] = b_n[p];
     }
   };
   auto logits = [&](const f32x16s (&pre)[2], int hg) {
@@ -221,7 +259,7 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
       float zp = 0.0f;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 ww = lds4(lf + F_W3 + q * 32 + 8 * g4 + 4 * h);
+        const float4 ww = lds4(lf + F_W3S + q * 32 + 8 * g4 + 4 * h);
         zp += relu(pre[rt][4 * g4 + 0]) * ww.x;
         zp += relu(pre[rt][4 * g4 + 1]) * ww.y;
         zp += relu(pre[rt][4 * g4 + 2]) * ww.z;
@@ -274,6 +312,9 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
         for (int u = 0; u < 4; ++u)
           mk[u] = pre[rt][4 * g4 + u] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
         *reinterpret_cast<bf16x4 *>(mki + (sbb ^ (16 * (4 * q + g4)))) = mk;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2 *>(mkh + (sbb ^ (16 * (4 * q + g4)))) =
+            __builtin_bit_cast(u32x2, mk) & 0x3C003C00u;
       }
       f32x16s t1 = lds_acc16(b1f, q * 32, h);
 #pragma unroll
@@ -310,7 +351,7 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
   };
   // ---- dH1 tile q of the half (transposed) -> relu' -> dW1 / db1 / items
   auto dH1 = [&](bool item_a) {
-    const int rb0 = opq(rb0_), rb1 = opq(rb1_), tq0 = opq(tq0_), tq1 = opq(tq1_);
+    const int rb0 = opq(rb0_), rb1 = opq(rb1_);
     const float *b1f = lf + F_B1F + (item_a ? 0 : kH1);
     const float b1T = b1f[q * 32 + lr];
     float sg = 0.0f;
@@ -320,19 +361,15 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
 #pragma unroll
       for (int j = 0; j < 16; ++j) dh[j] = 0.0f;
       const int rb = rt == 0 ? rb0 : rb1;
-      bf16x8 lo_c = ld_tr(w2dlo, tq0, tq1, 0), lo_n = lo_c;
-      bf16x8 m_c = ld_row(mki, rb, 0), m_n = m_c;
+      f16x8 m_c = __builtin_bit_cast(f16x8, ld_row(mkh, rb, 0)), m_n = m_c;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        if (s + 1 < 8) {
-          m_n = ld_row(mki, rb, s + 1);
-          lo_n = ld_tr(w2dlo, tq0, tq1, s + 1);
-        }
+        if (s + 1 < 8) m_n = __builtin_bit_cast(f16x8, ld_row(mkh, rb, s + 1));
         __builtin_amdgcn_sched_barrier(0);
-        const bf16x8 wa[3] = {wd[s][0], wd[s][1], lo_c};
-        dh = mfma_split3(m_c, wa, dh);
+        // S_D dH1 = M (S_D W2'): the mask is exact in f16
+        dh = mfma_f16(m_c, wd[s][1], dh);
+        dh = mfma_f16(m_c, wd[s][0], dh);
         m_c = m_n;
-        lo_c = lo_n;
       }
       // the transposed layer-1 tile (the same two-step chain as layer1())
       f32x16s tT;
@@ -493,15 +530,16 @@ __global__ __launch_bounds__(s128::kThreads, 1) void policy_train_split128_kerne
     const float s3 = half_sum32(accW3[j]);
     if (lr == 31) {
       slab[PL.ob2() + q * 32 + acc_row(j, h)] = s2 * lf[F_W3 + q * 32 + acc_row(j, h)];
-      slab[PL.ow3() + q * 32 + acc_row(j, h)] = s3;
+      slab[PL.ow3() + q * 32 + acc_row(j, h)] = s3 * (1.0f / S2);
     }
   }
   {
-    const float t0 = wf0 + __shfl_xor(wf0, 32, kWave);
-    const float t1 = wf1 + __shfl_xor(wf1, 32, kWave);
-    const float t2 = wf2 + __shfl_xor(wf2, 32, kWave);
-    const float va = sa + __shfl_xor(sa, 32, kWave);
-    const float vb = sb + __shfl_xor(sb, 32, kWave);
+    // dH1 was in units of S_D
+    const float t0 = (wf0 + __shfl_xor(wf0, 32, kWave)) * (1.0f / SD);
+    const float t1 = (wf1 + __shfl_xor(wf1, 32, kWave)) * (1.0f / SD);
+    const float t2 = (wf2 + __shfl_xor(wf2, 32, kWave)) * (1.0f / SD);
+    const float va = (sa + __shfl_xor(sa, 32, kWave)) * (1.0f / SD);
+    const float vb = (sb + __shfl_xor(sb, 32, kWave)) * (1.0f / SD);
     if (h == 0) {
       const int i = q * 32 + lr;
       slab[PL.oW1() + i * kF0 + 0] = t0;

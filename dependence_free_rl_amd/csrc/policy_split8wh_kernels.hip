@@ -130,8 +130,6 @@ typedef __attribute__((address_space(3))) bf16x8 lbf16x8;
 typedef __attribute__((address_space(3))) bf16x4 lbf16x4;
 typedef __attribute__((address_space(3))) s16x4 ls16x4;
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) f16x8 lf16x8;
 typedef __attribute__((address_space(3))) f16x4 lf16x4;
 
@@ -141,24 +139,11 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 __device__ __forceinline__ f32x4 mfma16h(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
-// x (already scaled) -> hi + lo, f16, round to nearest; x - hi is exact
-__device__ __forceinline__ void split2h(float x, _Float16 &hi, _Float16 &lo) {
-  hi = (_Float16)x;
-  lo = (_Float16)(x - (float)hi);
-}
 __device__ __forceinline__ f16x8 ld8h(int off) {
   return *(const lf16x8 *)(size_t)(unsigned)off;
 }
 __device__ __forceinline__ void st4h(int off, f16x4 v) {
   *(lf16x4 *)(size_t)(unsigned)off = v;
-}
-// 2^(14 - e) for a maximum m <= 2^e (frexp), e clamped so that products of
-// two scales and their inverses stay normal f32
-__device__ __forceinline__ float scale_for(float m) {
-  int e = 0;
-  (void)frexpf(m, &e);
-  e = min(max(e, -40), 40);
-  return ldexpf(1.0f, 14 - e);
 }
 // image accesses at absolute LDS byte addresses
 __device__ __forceinline__ bf16x8 ld8(int off) {
@@ -305,9 +290,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     const float MH = fmaxf(lf[F_SC + 0], lf[F_SC + 1]);
     __syncthreads();
     if (tid == 0) {
-      lf[F_SC + 0] = scale_for(MW);  // S_W
-      lf[F_SC + 1] = scale_for(MD);  // S_D
-      lf[F_SC + 2] = scale_for(MH);  // S_H
+      lf[F_SC + 0] = f16_scale_for(MW);  // S_W
+      lf[F_SC + 1] = f16_scale_for(MD);  // S_D
+      lf[F_SC + 2] = f16_scale_for(MH);  // S_H
     }
     __syncthreads();
   }

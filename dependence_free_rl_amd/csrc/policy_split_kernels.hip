@@ -560,7 +560,10 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
                                      hipStream_t s, KernelInfo *info) {
   if (info) info->math = kMathSplitTrain;
   if (a.env.B == kSplit128Bins) {
-    if (info) info->name = "policy_train_split128_kernel";
+    if (info) {
+      info->name = "policy_train_split128_kernel";
+      info->math = kMathSplitTrainF16;
+    }
     return launch_policy_train_split128(a, grid, s);
   }
   if (train_kernel_is("split8w")) {

@@ -287,7 +287,8 @@ enum Math {
   kMathF32Mfma = 0,       // f32-input MFMA (v_mfma_f32_32x32x2_f32) / f32 VALU
   kMathSplitTrain = 1,    // bf16 MFMA on 3-part splits: layer 2 six products per
                           // f32 product, dW2 / dH1 three (rank-1 backward)
-  kMathSplitRollout = 2,  // bf16 MFMA on 3-part splits: six products (layer 2)
+  kMathSplitRollout = 2,  // layer 2 on f16 pairs: three f16 products per f32
+                          // product (the other layers f32 MFMA)
   kMathSplitTrainF16 = 3  // layer 2 three f16 MFMAs per f32 product (scaled f16
                           // pairs), dH1 two, dW2 three bf16 (8 per 3 products)
 };

@@ -193,6 +193,61 @@ __device__ __forceinline__ void img_store_split(char *img_hi, char *img_mid,
   }
 }
 
+// ---- f16 pairs (policy_split8wh_kernels.hip, policy_split128_kernels.hip):
+// an operand with a bound known before the kernel is scaled by a power of
+// two S (|S x| <= 2^14, f16's range ends at 65504) and split EXACTLY into two
+// f16 parts,
+//     S x = hi + lo + e,  hi = f16(S x), lo = f16(S x - hi),  |e| <= 2^-22 |S x|
+// (11 significant bits per part, round to nearest; S x - hi is exact).  A
+// product of two f16 values is exact in f32, so a dot product is
+//     (S_a a).(S_b b) = hi.hi + hi.lo + lo.hi + d,  |d| <= 3 2^-22 sum|a_k b_k|
+// (the dropped lo.lo and the two e terms): three f16 MFMAs per K slice in
+// place of the bf16 split's six, two against an operand exact in f16 (a 0/1
+// mask) in place of three.  f16 and bf16 MFMAs run at the same rate.  The
+// result is in units of S_a S_b and is unscaled exactly (a power of two).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split2h(float x, _Float16 &hi, _Float16 &lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+// 2^(14 - e) for a maximum m <= 2^e (frexp); e clamped so that products of
+// two scales and their inverses stay normal f32
+__device__ __forceinline__ float f16_scale_for(float m) {
+  int e = 0;
+  (void)frexpf(m, &e);
+  e = min(max(e, -40), 40);
+  return ldexpf(1.0f, 14 - e);
+}
+__device__ __forceinline__ f32x16s mfma_f16(f16x8 a, f16x8 b, f32x16s c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// the bits of a bf16 0/1 operand as f16 (1.0 = 0x3F80 -> 0x3C00)
+__device__ __forceinline__ f16x8 mask_bf16_to_f16(bf16x8 m) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f16x8, __builtin_bit_cast(u32x4, m) & 0x3C003C00u);
+}
+// A 32x32 f32 tile in MFMA C layout (as img_store_split_b), times S, as two
+// f16 part images
+__device__ __forceinline__ void img_store_h2(char *img_hi, char *img_lo, int base,
+                                             int c0, const f32x16s &v, float S) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    f16x4 ph, pl;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      _Float16 a, b;
+      split2h(v[4 * g + u] * S, a, b);
+      ph[u] = a;
+      pl[u] = b;
+    }
+    const int off = base ^ (16 * ((c0 >> 3) + g));
+    *reinterpret_cast<f16x4 *>(img_hi + off) = ph;
+    *reinterpret_cast<f16x4 *>(img_lo + off) = pl;
+  }
+}
+
 // ---- helpers of the split train kernels (policy_split_kernels.hip,
 // policy_split128_kernels.hip)
 namespace split {

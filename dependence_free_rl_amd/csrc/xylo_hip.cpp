@@ -1178,15 +1178,17 @@ std::string kernel_json(const xh::KernelInfo &k) {
   // MFMA products per f32 product of the kernel's arithmetic (equal FLOPs
   // per GEMM): bf16 / f16 run at the same dense rate (MI355X_MICROARCH.md)
   const double prod = k.math == xh::kMathSplitTrain      ? 4.0
-                      : k.math == xh::kMathSplitRollout  ? 6.0
+                      : k.math == xh::kMathSplitRollout  ? 3.0
                       : k.math == xh::kMathSplitTrainF16 ? 8.0 / 3.0
                                                          : 0.0;
-  if (k.math == xh::kMathSplitTrainF16)
+  if (k.math == xh::kMathSplitTrainF16 || k.math == xh::kMathSplitRollout)
     std::snprintf(buf, sizeof buf,
-                  "{\"kernel\": \"%s\", \"math\": \"f16_pair_bf16_split\", "
+                  "{\"kernel\": \"%s\", \"math\": \"%s\", "
                   "\"bf16_products_per_f32_product\": null, "
                   "\"products_per_f32_product\": %.6g, \"peak_tflops\": %.6g}",
-                  k.name, prod, kBf16DensePeakTflops / prod);
+                  k.name,
+                  k.math == xh::kMathSplitRollout ? "f16_pair" : "f16_pair_bf16_split",
+                  prod, kBf16DensePeakTflops / prod);
   else if (prod > 0)
     std::snprintf(buf, sizeof buf,
                   "{\"kernel\": \"%s\", \"math\": \"bf16_split\", "

@@ -118,7 +118,8 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
         assert kt["math"] == "f16_pair_bf16_split"
         assert kt["products_per_f32_product"] == pytest.approx(prod, rel=1e-5)
         assert kt["peak_tflops"] == pytest.approx(2500.0 / prod, rel=1e-5)
-        assert kr["peak_tflops"] == pytest.approx(2500.0 / 6)
+        assert kr["math"] == "f16_pair"
+        assert kr["peak_tflops"] == pytest.approx(2500.0 / 3)
     else:
         assert kt["math"] == "f32_mfma" and kt["peak_tflops"] == 157.3
         assert kt["kernel"].startswith("policy_train")
