@@ -537,7 +537,10 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 // (policy_split8wh_kernels.hip); =split8wp keeps its all-bf16 form
 // (policy_split8wp_kernels.hip), =split4p the pipelined 4-wave one
 // (policy_split4p_kernels.hip), =split8w the unpipelined 8-wave one
-// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel.
+// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel; for
+// the 128-bin 3-D shape the default is the pipelined 8-wave kernel
+// (policy_split8x_kernels.hip) and =split128 keeps the 4-wave one
+// (policy_split128_kernels.hip).
 // Diagnostic overrides, read per launch and reported by
 // xh_trainer_kernel_info.
 bool train_split_enabled() {
@@ -560,10 +563,12 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
                                      hipStream_t s, KernelInfo *info) {
   if (info) info->math = kMathSplitTrain;
   if (a.env.B == kSplit128Bins) {
-    if (info) {
-      info->name = "policy_train_split128_kernel";
-      info->math = kMathSplitTrainF16;
+    if (info) info->math = kMathSplitTrainF16;
+    if (!train_kernel_is("split128")) {
+      if (info) info->name = "policy_train_split8x_kernel";
+      return launch_policy_train_split8x(a, grid, s);
     }
+    if (info) info->name = "policy_train_split128_kernel";
     return launch_policy_train_split128(a, grid, s);
   }
   if (train_kernel_is("split8w")) {

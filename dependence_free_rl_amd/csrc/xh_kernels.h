@@ -319,6 +319,8 @@ hipError_t launch_policy_train_split4p(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
+hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
                               hipStream_t s);
