@@ -634,9 +634,10 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
 // 4h + (e&3) for element e of lane half h.  W2 is staged with the columns
 // of every 16-block permuted to that order (bits 2 and 3 of the column
 // swapped), so each A fragment is one ds_read_b128 of the swizzled image.
-// The pre-activations stay in units of S_W S_H: b2 is staged times that and
-// w3 divided by it, so relu(pre + b2) w3 takes the same roundings as the
-// unscaled values.  The logits differ from rollout_wave_kernel's in the
+// Layer 1 is staged times S_H (weights and bias: its output is S_H H1
+// exactly), b2 times S_W S_H as layer 2's C input and w3 divided by it, so
+// the partial logits take the same roundings as unscaled values; both
+// biases enter as the MFMA chains' C inputs.  The logits differ from rollout_wave_kernel's in the
 // last places (f32-class: tests/test_gpu_scale.py); the sampler, the env
 // step and everything after are the same code.
 // LDS (bytes): two W2 part images [o][permuted i] (64 KB), then f32 W1
@@ -695,9 +696,12 @@ __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
     *reinterpret_cast<_Float16 *>(lds + L::W2 + off) = x0;
     *reinterpret_cast<_Float16 *>(lds + L::W2 + 128 * kImgRow + off) = x1;
   }
-  for (int i = threadIdx.x; i < S::H1 * S::F0; i += blockDim.x) lf[L::W1 + i] = P[PL.oW1() + i];
+  // layer 1 staged times S_H (its output is H1 S_H exactly: a power of two),
+  // b2 times S_W S_H (layer 2's C input), w3 divided by it
+  for (int i = threadIdx.x; i < S::H1 * S::F0; i += blockDim.x)
+    lf[L::W1 + i] = P[PL.oW1() + i] * SH;
   for (int i = threadIdx.x; i < S::H1; i += blockDim.x) {
-    lf[L::B1 + i] = P[PL.ob1() + i];
+    lf[L::B1 + i] = P[PL.ob1() + i] * SH;
     lf[L::B2 + i] = P[PL.ob2() + i] * S2;
     lf[L::W3 + i] = P[PL.ow3() + i] * (1.0f / S2);
   }
@@ -717,21 +721,36 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
   const float *lf = reinterpret_cast<const float *>(lds + L::F);
   const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
   const char *w2i[2] = {lds + L::W2, lds + L::W2 + 128 * kImgRow};
-  const float SH = lf[L::SH];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     float xb[S::S1];
 #pragma unroll
     for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
+    // layer 2's accumulators start at b2 S_W S_H (C layout: register 4q + u
+    // = feature ot*32 + 8q + 4h + u)
     f32x16s pre[4];
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) pre[ot][j] = 0.0f;
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
+        pre[ot][4 * q + 0] = bb.x;
+        pre[ot][4 * q + 1] = bb.y;
+        pre[ot][4 * q + 2] = bb.z;
+        pre[ot][4 * q + 3] = bb.w;
+      }
 #pragma unroll 1
     for (int it = 0; it < 4; ++it) {
-      // layer-1 tile it: chain, + bias, relu (as rollout_wave_kernel)
-      f32x16 t1 = zero16();
+      // layer-1 tile it, times S_H: the bias as the chain's C input, relu
+      f32x16 t1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
+        t1[4 * q + 0] = bb.x;
+        t1[4 * q + 1] = bb.y;
+        t1[4 * q + 2] = bb.z;
+        t1[4 * q + 3] = bb.w;
+      }
 #pragma unroll
       for (int s1 = 0; s1 < S::S1; ++s1) {
         const int k = 2 * s1 + h;
@@ -740,18 +759,11 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
       }
       f16x8 bfr[2][2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
-        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float v = relu(t1[4 * q + u] + bq[u]);
-          _Float16 p0, p1;
-          split2h(v * SH, p0, p1);
-          const int j = 4 * q + u;
-          bfr[j >> 3][0][j & 7] = p0;
-          bfr[j >> 3][1][j & 7] = p1;
-        }
+      for (int j = 0; j < 16; ++j) {
+        _Float16 p0, p1;
+        split2h(relu(t1[j]), p0, p1);
+        bfr[j >> 3][0][j & 7] = p0;
+        bfr[j >> 3][1][j & 7] = p1;
       }
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot) {
@@ -776,12 +788,10 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
       float zp = 0.0f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
         const float4 ww = *reinterpret_cast<const float4 *>(lf + L::W3 + ot * 32 + 8 * q + 4 * h);
-        const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
         const float wq[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) zp += relu(pre[ot][4 * q + u] + bq[u]) * wq[u];
+        for (int u = 0; u < 4; ++u) zp = fmaf(relu(pre[ot][4 * q + u]), wq[u], zp);
       }
       z += zp + __shfl_xor(zp, 32, kWave);
     }

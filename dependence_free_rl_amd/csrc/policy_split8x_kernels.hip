@@ -132,6 +132,18 @@ __device__ __forceinline__ f32x4 lds4v(const float *p) {
 __device__ __forceinline__ float relu(float x) {
   return __int_as_float(max(__float_as_int(x), 0));
 }
+// relu'(x) in {0, 1} from x's bits: v_med3_i32(bits, 0, 1) (a compare would
+// write VCC, and its consumer would wait the VCC hazard's s_nop)
+__device__ __forceinline__ int relu_bit(float x) {
+  int m;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m) : "v"(__float_as_int(x)));
+  return m;
+}
+// the integer relu masks of policy_split8wh_kernels.hip: here the inline asm
+// costs 74 spilled registers (4.88 -> 33.6 ms per epoch): off
+#ifndef XH_8X_IMASK
+#define XH_8X_IMASK 0
+#endif
 // sum over the four lane groups (rows of 16 lanes) without an LDS round
 // trip: ((g0 + g1) + (g2 + g3)) in every lane, as two __shfl_xor steps
 __device__ __forceinline__ float sum_groups(float v) {
@@ -526,7 +538,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float pv = pre_v[rt][jj];
+#if XH_8X_IMASK
+          const float gm = gr4[rt] * (float)relu_bit(pv);
+#else
           const float gm = pv > 0.0f ? gr4[rt] : 0.0f;
+#endif
           accW3[jj] = fmaf(gm, pv, accW3[jj]);
           accB2[jj] += gm;
         }
@@ -544,14 +560,23 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
       } else if (k >= 20 && k < 24) {
         // the relu masks of r-tile k - 20 -> the bf16 and f16 mask images
         const int rt = k - 20;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#if XH_8X_IMASK
+        unsigned m[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_v[rt][jj]);
+        const u32x2 mm = {m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm * 0x3F80u));
+        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm * 0x3C00u));
+#else
         bf16x4 mk;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
           mk[jj] = pre_v[rt][jj] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
         st4(stb + L_MASK + 4096 * rt, mk);
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         const u32x2 mb = __builtin_bit_cast(u32x2, mk) & 0x3C003C00u;
         st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mb));
+#endif
       } else if (k == 36) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 44) {
