@@ -1,0 +1,707 @@
+// policy_split4h_kernels.hip -- the PPO / actor-critic train epoch of the
+// 32-bin 1-D [64,64] policy (BASELINE config 2): the pipelined kernel of
+// policy_split8wh_kernels.hip (f16 pairs for layer 2 and dH1, the exact
+// bf16 split for dW2, rank-1 backward; see its header and xh_split.h) for
+// 64 features and 64-row groups of two 32-bin envs.
+//
+// Four waves per workgroup, wave w owning features 16 w .. 16 w + 15 of every
+// product, two workgroups per CU (two waves per SIMD, 256 registers each).
+// Per group: layer 2 24 f16 MFMAs per wave (K = 64: two K-slices), dW2 24
+// bf16, dH1 16 f16.  The two envs of a group are rows 0-31 and 32-63: the
+// softmax and its sums run over 32-lane segments, each env has its record
+// (action, old probability, advantage) and its item -- the layer-1 bias
+// (item folded in) is chosen per r-tile, the dW1 item sums per env.
+//
+//   X(j): MFMA layer 2 of group j+1 | VALU softmax + g of group j, masks,
+//         dW3 / db2, g (x) H1 of K-step 0 (env A's rows); group j+1's
+//         partial logits                                     -> barrier
+//   Y(j): MFMA dW2 and dH1 of group j | VALU g (x) H1 of K-step 1 (env B's
+//         rows), layer 1 of group j+2, dW1 of group j        -> barrier
+//
+// Images keep the 256-byte rows (and swizzles) of the 128-feature kernels
+// with 64 features used.
+#include <cstdlib>
+
+#include "xh_device.h"
+#include "xh_kernels.h"
+#include "xh_split.h"
+
+namespace xh {
+namespace s4h {
+
+constexpr int kD = 1, kF0 = 2 * kD, kH = 64;
+constexpr int kNW = 4;                   // waves
+constexpr int kThreads = 64 * kNW;
+constexpr int kImg = 64 * kImgRow;       // one 64-row part image, 16 KB
+constexpr int L_H1 = 0;                  // H1 as two f16 parts (S_H)
+constexpr int L_MASK = 2 * kImg;         // bf16 mask (dW2's A operand)
+constexpr int L_MASKH = 3 * kImg;        // f16 mask (dH1's A operand)
+constexpr int L_F = 4 * kImg;
+constexpr int F_W1T = 0;                 // [64 i]: W1[i][0], the bin column
+constexpr int F_B1F = F_W1T + kH;        // [2 items][64]: b1 + the item's part
+constexpr int F_B2 = F_B1F + 2 * kH;     // [64] b2 S_W S_H
+constexpr int F_W3 = F_B2 + kH;          // [64] w3 / (S_W S_H)
+constexpr int F_B3 = F_W3 + kH;          // [4]
+constexpr int F_Z = F_B3 + 4;            // [2 parity][64 rows][4 waves] partial logits
+constexpr int F_GW = F_Z + 2 * 64 * kNW; // [4 waves][64 rows] g, row order
+constexpr int F_GP = F_GW + kNW * 64;    // [4 waves][16 li][4 rt] g, C-layout order
+constexpr int F_X = F_GP + kNW * 64;     // [3 slots][64 rows] bins / 8
+constexpr int F_XP = F_X + 3 * 64;       // [3 slots][16 li][4 rt]
+constexpr int F_IT = F_XP + 3 * 64;      // [3 slots][2 envs] item is item_a (+ pad)
+constexpr int F_REC = F_IT + 8;          // [3 slots][2 envs][action, pold, adv, -]
+constexpr int F_SC = F_REC + 3 * 8;      // [16] the scales' reduction
+constexpr int F_END = F_SC + 16;
+constexpr size_t kLds = L_F + sizeof(float) * F_END;
+static_assert(2 * kLds <= 160 * 1024, "LDS: two workgroups per CU");
+static_assert(F_REC % 4 == 0 && F_GW % 4 == 0 && F_GP % 4 == 0 && F_X % 4 == 0 &&
+                  F_XP % 4 == 0 && F_Z % 4 == 0 && F_W1T % 4 == 0 && F_B1F % 4 == 0 &&
+                  F_B2 % 4 == 0 && F_W3 % 4 == 0,
+              "16-byte aligned f32 vectors");
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x8 lbf16x8;
+typedef __attribute__((address_space(3))) bf16x4 lbf16x4;
+typedef __attribute__((address_space(3))) s16x4 ls16x4;
+
+typedef __attribute__((address_space(3))) f16x8 lf16x8;
+typedef __attribute__((address_space(3))) f16x4 lf16x4;
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16h(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16x8 ld8h(int off) {
+  return *(const lf16x8 *)(size_t)(unsigned)off;
+}
+__device__ __forceinline__ void st4h(int off, f16x4 v) {
+  *(lf16x4 *)(size_t)(unsigned)off = v;
+}
+// image accesses at absolute LDS byte addresses
+__device__ __forceinline__ bf16x8 ld8(int off) {
+  return *(const lbf16x8 *)(size_t)(unsigned)off;
+}
+__device__ __forceinline__ void st4(int off, bf16x4 v) {
+  *(lbf16x4 *)(size_t)(unsigned)off = v;
+}
+// two ds_read_b64_tr_b16 (EXEC full): elements 0-3 from o0, 4-7 from o1
+__device__ __forceinline__ bf16x8 ldtr(int o0, int o1) {
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4 *)(size_t)(unsigned)o0);
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4 *)(size_t)(unsigned)o1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// the images' swizzle: chunk ^= swz2(row & 15)
+__device__ __forceinline__ constexpr int swz2(int r) {
+  return ((r & 7) << 1) ^ ((r & 8) ? 9 : 0);
+}
+__device__ __forceinline__ int ioff2(int row, int ch) {
+  return kImgRow * row + 16 * (ch ^ swz2(row & 15));
+}
+// row reads: lane (G, li) reads row 16 rt + li, chunk 4s + G at
+// (rd_base ^ 64 s) + 4096 rt
+__device__ __forceinline__ int rd_base(int G, int li) {
+  return kImgRow * li + 16 * (G ^ swz2(li));
+}
+// dW2's A operand M^T by transposed reads: K-step ks element j of lane group
+// G is row 32 ks + 4G + j (j < 4) or 32 ks + 16 + 4G + j - 4 (the T layout's
+// r-tiles 2 ks, 2 ks + 1); read t: lane 4q + p supplies row 16t + 4G + q,
+// columns 16 ot + 4p .. +3, at (trm_base(t) ^ 32 ot) + 8192 ks
+__device__ __forceinline__ int trm_base(int l, int t) {
+  const int G = l >> 4, li = l & 15, q = li >> 2, p = li & 3;
+  const int row = 16 * t + 4 * G + q;
+  return kImgRow * row + 16 * ((p >> 1) ^ swz2(row & 15)) + 8 * (p & 1);
+}
+// stores from the C layout (row 16 rt + li, features 16 ft + 4G .. +3):
+// (st_base ^ 32 ft) + 4096 rt
+__device__ __forceinline__ int st_base(int G, int li) {
+  return kImgRow * li + 16 * ((G >> 1) ^ swz2(li)) + 8 * (G & 1);
+}
+__device__ __forceinline__ f32x4 lds4v(const float *p) {
+  return *reinterpret_cast<const f32x4 *>(p);
+}
+__device__ __forceinline__ float relu(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+// relu'(x) in {0, 1} from x's bits: v_med3_i32(bits, 0, 1) (a compare would
+// write VCC, and its consumer would wait the VCC hazard's s_nop)
+__device__ __forceinline__ int relu_bit(float x) {
+  int m;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m) : "v"(__float_as_int(x)));
+  return m;
+}
+// sum over the four lane groups (rows of 16 lanes) without an LDS round
+// trip: ((g0 + g1) + (g2 + g3)) in every lane, as two __shfl_xor steps
+__device__ __forceinline__ float sum_groups(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+#define FENCE() __builtin_amdgcn_sched_barrier(0)
+
+__global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
+    PolicyTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float *lf = reinterpret_cast<float *>(lds + L_F);
+  const PolicyLayout PL{kF0, kH, kH};
+  const float *P = a.params;
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+  const int l = tid & 63, G = l >> 4, li = l & 15;
+  const int ngroups = a.b.T * a.b.N / 2;  // 64-row groups of two envs
+  const int J = (int)blockIdx.x < ngroups
+                    ? (ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x
+                    : 0;
+  if (J == 0) return;  // uniform over the workgroup
+  int gstep = (int)gridDim.x;
+  // group index of this workgroup's group j (clamped: work past the end is
+  // discarded); its envs are transitions 2 g and 2 g + 1 of the [T][N] arrays
+  auto gindex = [&](int j) {
+    return (size_t)((int)blockIdx.x + min(j, J - 1) * gstep);
+  };
+
+  // ---- prologue: the scales (every workgroup the same), small parameters,
+  // the W2 / W2' fragments of tile w as f16 pairs
+  {
+    float mw = 0.0f, md = 0.0f, mh = 0.0f;
+    for (int e = tid; e < kH * kH; e += kThreads) {
+      const float v = P[PL.oW2() + e];
+      mw = fmaxf(mw, fabsf(v));
+      md = fmaxf(md, fabsf(v * P[PL.ow3() + e / kH]));
+    }
+    if (tid < kH) {
+      const float wv = P[PL.oW1() + tid * kF0 + kD];
+      const float ba = P[PL.ob1() + tid] + wv * ((float)a.env.item_a[0] / (float)kCapacity);
+      const float bb = P[PL.ob1() + tid] + wv * ((float)a.env.item_b[0] / (float)kCapacity);
+      mh = fabsf(P[PL.oW1() + tid * kF0]) + fmaxf(fabsf(ba), fabsf(bb));
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      mw = fmaxf(mw, __shfl_xor(mw, o, kWave));
+      md = fmaxf(md, __shfl_xor(md, o, kWave));
+      mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    }
+    if (l == 0) {
+      lf[F_SC + w] = mw;
+      lf[F_SC + 4 + w] = md;
+      lf[F_SC + 8 + w] = mh;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float MW = 0.0f, MD = 0.0f, MH = 0.0f;
+#pragma unroll
+      for (int v = 0; v < kNW; ++v) {
+        MW = fmaxf(MW, lf[F_SC + v]);
+        MD = fmaxf(MD, lf[F_SC + 4 + v]);
+        MH = fmaxf(MH, lf[F_SC + 8 + v]);
+      }
+      lf[F_SC + 12] = f16_scale_for(MW);  // S_W
+      lf[F_SC + 13] = f16_scale_for(MD);  // S_D
+      lf[F_SC + 14] = f16_scale_for(MH);  // S_H
+    }
+    __syncthreads();
+  }
+  const float SW = lf[F_SC + 12], SD = lf[F_SC + 13], SH = lf[F_SC + 14];
+  const float S2 = SW * SH;  // layer 2's pre-activations are in units of S2
+  for (int i = tid; i < kH; i += kThreads) {
+    lf[F_W1T + i] = P[PL.oW1() + i * kF0];
+    lf[F_B2 + i] = P[PL.ob2() + i] * S2;
+    lf[F_W3 + i] = P[PL.ow3() + i] * (1.0f / S2);
+  }
+  for (int e = tid; e < 2 * kH; e += kThreads) {
+    const int it = e / kH, u = e - it * kH;
+    const int *item = it == 0 ? a.env.item_a : a.env.item_b;
+    lf[F_B1F + e] = P[PL.ob1() + u] +
+                    P[PL.oW1() + u * kF0 + kD] * ((float)item[0] / (float)kCapacity);
+  }
+  if (tid == 0) lf[F_B3] = P[PL.ob3()];
+  f16x8 wl[2][2], wd[2][2];
+  const int rdb0 = rd_base(G, li);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float4 *src = reinterpret_cast<const float4 *>(
+        P + PL.oW2() + (16 * w + li) * kH + 32 * s + 8 * G);
+    const float4 v0 = src[0], v1 = src[1];
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 x0, x1;
+      split2h(v[j] * SW, x0, x1);
+      wl[s][0][j] = x0;
+      wl[s][1][j] = x1;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = 32 * s + 8 * G + j, col = 16 * w + li;
+      _Float16 x0, x1;
+      split2h((P[PL.oW2() + o * kH + col] * P[PL.ow3() + o]) * SD, x0, x1);
+      wd[s][0][j] = x0;
+      wd[s][1][j] = x1;
+    }
+  }
+  const int trm00 = trm_base(l, 0), trm10 = trm_base(l, 1);  // ^ 32 ot, + L_MASK
+  const int stb0 = st_base(G, li) ^ (32 * w);  // + L_H1 / L_MASK + 4096 rt
+  const int fo = 16 * w + 4 * G;  // this lane's 4 features in the C layout
+  float *gw = lf + F_GW + 64 * w;  // this wave's copies of the rows' g
+  float *gp = lf + F_GP + 64 * w;
+
+  f32x4 accW2[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accW2[ot][j] = 0.0f;
+  float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float accB3 = 0.0f, w0 = 0.0f, sa = 0.0f, sb = 0.0f;
+
+  // wave 0 stages group j+2 during X(j): branch-free loads at its start
+  // (lane = row: its bin; lanes 0-2 / 3-5 env A's / B's action, old
+  // probability and advantage, lanes 6 / 7 their items), the stores late
+  struct Raw {
+    int bi, rec;
+  };
+  auto stage_load = [&](int j) {
+    const size_t g = gindex(j);
+    int lo = l;
+    asm volatile("" : "+v"(lo));
+    const int bins = (int)*reinterpret_cast<const signed char *>(a.b.bins + g * 64 + lo);
+    const size_t ti = 2 * g + (l >= 3 && l != 6);
+    const int k = l % 3;
+    const int *src = l >= 6   ? reinterpret_cast<const int *>(a.b.items + (2 * g + (l & 1)) * 4)
+                     : k == 0 ? a.b.action + ti
+                     : k == 1 ? reinterpret_cast<const int *>(a.b.pold + ti)
+                              : reinterpret_cast<const int *>(a.adv + ti);
+    return Raw{bins, *src};
+  };
+  auto stage_store = [&](const Raw &r, int s) {
+    const float x = (float)r.bi / (float)kCapacity;
+    lf[F_X + s * 64 + l] = x;
+    lf[F_XP + s * 64 + 4 * (l & 15) + (l >> 4)] = x;
+    const int itA = __builtin_amdgcn_readlane(r.rec, 6);
+    const int itB = __builtin_amdgcn_readlane(r.rec, 7);
+    if (l == 0) {
+      lf[F_IT + 2 * s] = (signed char)(itA & 0xff) == a.env.item_a[0] ? 1.0f : 0.0f;
+      lf[F_IT + 2 * s + 1] = (signed char)(itB & 0xff) == a.env.item_a[0] ? 1.0f : 0.0f;
+    }
+    if (l < 6) lf[F_REC + 8 * s + (l >= 3 ? 4 + l - 3 : l)] = __int_as_float(r.rec);
+  };
+  // H1 values (C layout, r-tile rt) scaled by S_H -> the two f16 part images
+  auto store_h1 = [&](const f32x4 &t, int sb, int rt) {
+    f16x4 ph, pl;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      _Float16 x0, x1;
+      split2h(t[u] * SH, x0, x1);
+      ph[u] = x0;
+      pl[u] = x1;
+    }
+    st4h(sb + L_H1 + 4096 * rt, ph);
+    st4h(sb + L_H1 + kImg + 4096 * rt, pl);
+  };
+  // the layer-1 bias row (item folded in) of env e of the group in slot s
+  auto b1row = [&](int s, int e) {
+    const bool ia = __builtin_amdgcn_readfirstlane(__float_as_int(lf[F_IT + 2 * s + e])) != 0;
+    return lf + F_B1F + (ia ? 0 : kH);
+  };
+  // layer 1 (C layout) of the group in slot s, all four r-tiles -> H1 image
+  auto layer1_all = [&](int s, int stb) {
+    const f32x4 wa = lds4v(lf + F_W1T + fo);
+    const f32x4 bbA = lds4v(b1row(s, 0) + fo), bbB = lds4v(b1row(s, 1) + fo);
+    const f32x4 x0 = lds4v(lf + F_XP + s * 64 + 4 * li);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      const f32x4 &bb = rt < 2 ? bbA : bbB;
+      f32x4 t;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[j] = relu(fmaf(x0[rt], wa[j], bb[j]));
+      store_h1(t, stb, rt);
+    }
+  };
+  // layer 2 of the group whose H1 is in the image: 8 steps of 3 f16 MFMAs,
+  // task(k) after each MFMA (k = 0 .. 23)
+  auto layer2 = [&](int rdb, f32x4 (&pre)[4], auto &&task) {
+    const f32x4 b2 = lds4v(lf + F_B2 + fo);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) pre[rt] = b2;
+    f16x8 b_c[2], b_n[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) b_c[p] = ld8h(rdb + L_H1 + p * kImg);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int s = st >> 2, rt = st & 3;
+      if (st + 1 < 8) {
+        const int s1 = (st + 1) >> 2, r1 = (st + 1) & 3;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          b_n[p] = ld8h((rdb ^ (64 * s1)) + L_H1 + p * kImg + 4096 * r1);
+      }
+      FENCE();
+      pre[rt] = mfma16h(wl[s][1], b_c[0], pre[rt]);
+      FENCE();
+      task(3 * st);
+      FENCE();
+      pre[rt] = mfma16h(wl[s][0], b_c[1], pre[rt]);
+      FENCE();
+      task(3 * st + 1);
+      FENCE();
+      pre[rt] = mfma16h(wl[s][0], b_c[0], pre[rt]);
+      FENCE();
+      task(3 * st + 2);
+      FENCE();
+#pragma unroll
+      for (int p = 0; p < 2; ++p) b_c[p] = b_n[p];
+    }
+  };
+  // partial logits of rows 16 rt + li over this wave's features -> F_Z[zs]
+  auto partials = [&](const f32x4 (&pre)[4], const f32x4 &w3, int zs) {
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      float zp = relu(pre[rt][0]) * w3[0];
+      zp = fmaf(relu(pre[rt][1]), w3[1], zp);
+      zp = fmaf(relu(pre[rt][2]), w3[2], zp);
+      zp = fmaf(relu(pre[rt][3]), w3[3], zp);
+      zp = sum_groups(zp);
+      if (G == 0) lf[F_Z + zs * 256 + (16 * rt + li) * kNW + w] = zp;
+    }
+  };
+  auto no_task = [](int) {};
+
+  // ---- pipeline prologue: groups 0 and 1 staged, layer 1 and layer 2 of
+  // group 0 (its partial logits), layer 1 of group 1
+  f32x4 pre_cur[4];
+  Raw raw = {0, 0};
+  if (w == 0) {
+    stage_store(stage_load(0), 0);
+    stage_store(stage_load(1), 1);
+  }
+  __syncthreads();
+  layer1_all(0, stb0);
+  __syncthreads();
+  layer2(rdb0, pre_cur, no_task);
+  partials(pre_cur, lds4v(lf + F_W3 + fo), 0);
+  __syncthreads();
+  layer1_all(1, stb0);
+  __syncthreads();
+
+  for (int j = 0; j < J; ++j) {
+    const int cs = j % 3, ns = (j + 2) % 3;  // slots of groups j and j + 2
+    int rdb = rdb0, trm0 = trm00, trm1 = trm10, stb = stb0;
+    asm volatile("" : "+v"(rdb), "+v"(trm0), "+v"(trm1), "+v"(stb), "+s"(gstep));
+    if (w == 0) raw = stage_load(j + 2);
+    const float *xim = lf + F_X + cs * 64;
+    const float w1a = lf[F_W1T + 16 * w + li];  // T layout: feature 16 w + li
+
+    // ================= X(j): layer 2 of group j+1 with group j's VALU ====
+    const f32x4 z4 = lds4v(lf + F_Z + (j & 1) * 256 + kNW * l);
+    const float b3 = lf[F_B3];
+    const f32x4 recA = lds4v(lf + F_REC + 8 * cs), recB = lds4v(lf + F_REC + 8 * cs + 4);
+    const float itA = lf[F_IT + 2 * cs], itB = lf[F_IT + 2 * cs + 1];
+    f32x4 gx0[2];
+    float ex = 0.0f, se = 0.0f, gz = 0.0f;
+    f32x4 gr4, ggk[2], hT[2];
+    bf16x8 bq0[3];
+    bool iaA = false, iaB = false;
+    float b1tA = 0.0f, b1tB = 0.0f;
+    f32x4 w3;
+    auto xtask = [&](int k) {
+      if (k == 0) {
+        ex = __expf(((z4[0] + z4[1]) + (z4[2] + z4[3])) + b3);
+      } else if (k == 1) {
+        se = seg_sum<32>(ex);  // per env (32-lane segment)
+      } else if (k == 2) {
+        const int cA = __builtin_amdgcn_readfirstlane(__float_as_int(recA[0]));
+        const int cB = __builtin_amdgcn_readfirstlane(__float_as_int(recB[0]));
+        const bool eB = l >= 32;
+        const float p = ex * __builtin_amdgcn_rcpf(se);
+        const float pcA = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), cA));
+        const float pcB = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 32 + cB));
+        const int c = eB ? cB : cA;
+        const float pc = eB ? pcB : pcA;
+        const float Ac = __int_as_float(__builtin_amdgcn_readfirstlane(
+                             __float_as_int(recA[2]))) * (eB ? 0.0f : 1.0f) +
+                         __int_as_float(__builtin_amdgcn_readfirstlane(
+                             __float_as_int(recB[2]))) * (eB ? 1.0f : 0.0f);
+        if (a.algo == kPPO) {
+          // clipped_gradient (rl.h:54-74) through softmax_layer::backward
+          const float poA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(recA[1])));
+          const float poB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(recB[1])));
+          const float po = eB ? poB : poA;
+          const float ratio = pc * __builtin_amdgcn_rcpf(po);
+          float ce = a.clip_eps;
+          asm volatile("" : "+s"(ce));
+          const float clipped = fminf(fmaxf(ratio, 1.0f - ce), 1.0f + ce);
+          const float ig = fminf(clipped * Ac, ratio * Ac) * -1.0f;
+          const float gc = ig * __builtin_amdgcn_rcpf(pc);
+          const float lin = (l & 31) == c ? p : 0.0f;
+          gz = (lin - p * pc) * gc;
+        } else {
+          // softmax_gradient_log (rl.h:45-52) through softmax-xent
+          gz = p * Ac;
+          if ((l & 31) == c) gz -= Ac;
+        }
+      } else if (k == 3) {
+        gw[l] = gz;
+        gp[4 * (l & 15) + (l >> 4)] = gz;
+        accB3 += gz;  // wave 0's is written out
+        iaA = __builtin_amdgcn_readfirstlane(__float_as_int(itA)) != 0;
+        iaB = __builtin_amdgcn_readfirstlane(__float_as_int(itB)) != 0;
+        b1tA = lf[F_B1F + (iaA ? 0 : kH) + 16 * w + li];
+        b1tB = lf[F_B1F + (iaB ? 0 : kH) + 16 * w + li];
+        // the rows of K-step 0 (env A; T layout)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) gx0[h] = lds4v(xim + 16 * h + 4 * G);
+      } else if (k == 4) {
+        gr4 = lds4v(gp + 4 * li);  // g of rows 16 rt + li
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ggk[h] = lds4v(gw + 16 * h + 4 * G);
+      } else if (k == 6 || k == 7) {
+        const int h = k - 6;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) hT[h][jj] = relu(fmaf(gx0[h][jj], w1a, b1tA));
+      } else if (k >= 8 && k < 12) {
+        // dW3 / db2 of r-tile rt (pre-activations in units of S2)
+        const int rt = k - 8;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float v = pre_cur[rt][jj];
+          const float gm = gr4[rt] * (float)relu_bit(v);
+          accW3[jj] = fmaf(gm, v, accW3[jj]);
+          accB2[jj] += gm;
+        }
+      } else if (k >= 12 && k < 16) {
+        // g (x) H1 of K-step 0, two values per slot
+        const int h = (k - 12) >> 1, j0 = 2 * ((k - 12) & 1);
+#pragma unroll
+        for (int jj = j0; jj < j0 + 2; ++jj) {
+          __bf16 p0, p1, p2;
+          split3(hT[h][jj] * ggk[h][jj], p0, p1, p2);
+          bq0[0][4 * h + jj] = p0;
+          bq0[1][4 * h + jj] = p1;
+          bq0[2][4 * h + jj] = p2;
+        }
+      } else if (k >= 16 && k < 20) {
+        // the relu masks of r-tile k - 16 -> the bf16 and f16 mask images
+        const int rt = k - 16;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        unsigned m[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
+        const u32x2 mm = {m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm * 0x3F80u));
+        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm * 0x3C00u));
+      } else if (k == 20) {
+        w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
+      } else if (k == 22) {
+        if (w == 0) stage_store(raw, ns);  // group j+2's rows
+      }
+    };
+    f32x4 pre_nx[4];
+    layer2(rdb, pre_nx, xtask);
+    partials(pre_nx, w3, (j + 1) & 1);
+    __syncthreads();
+
+    // ================= Y(j): dW2 / dH1 of group j with VALU of j, j+2 =====
+    // 16 blocks: b < 4 dW2 of K-step 0 (ot = b), three bf16 MFMAs; 4 <= b <
+    // 12 dH1, two f16 MFMAs (rt = (b - 4) / 2, s = (b - 4) % 2); b >= 12 dW2
+    // of K-step 1 (its operand is built in blocks 2-5); operands one block
+    // ahead
+    {
+      float sgA = 0.0f, sgB = 0.0f;
+      bf16x8 bq1[3];
+      f32x4 rx0[2], rgg[2], hT1[2];
+      f32x4 wa, bbA, bbB, xp0, t1;
+      float itnA = 0.0f, itnB = 0.0f;
+      f32x4 dx0, dgg;
+      f32x4 dh[2];
+      auto load_ops = [&](int b, bf16x8 &A) {
+        if (b < 4 || b >= 12) {
+          const int ks = b >= 12, ot = b & 3;
+          A = ldtr((trm0 ^ (32 * ot)) + L_MASK + 8192 * ks,
+                   (trm1 ^ (32 * ot)) + L_MASK + 8192 * ks);
+        } else {
+          const int rt = (b - 4) >> 1, s = (b - 4) & 1;
+          A = ld8((rdb ^ (64 * s)) + L_MASKH + 4096 * rt);  // f16 bits
+        }
+      };
+      // dW1 / db1 / item sums of value jj of r-tile rt (T layout; r-tiles 0,
+      // 1 env A, 2, 3 env B)
+      auto dw1 = [&](int jj, int rt) {
+        const int q = rt & 1;
+        const float tT = fmaf(dx0[jj], w1a, rt < 2 ? b1tA : b1tB);
+        const float d = tT > 0.0f ? dh[q][jj] * dgg[jj] : 0.0f;
+        if (rt < 2)
+          sgA += d;
+        else
+          sgB += d;
+        w0 = fmaf(d, dx0[jj], w0);
+      };
+      auto ytask = [&](int b) {
+        if (b == 0) {
+          // rows of K-step 1 (env B; T layout) and their g; group j+2's items
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int r0 = 32 + 16 * h + 4 * G;
+            rx0[h] = lds4v(xim + r0);
+            rgg[h] = lds4v(gw + r0);
+          }
+          itnA = lf[F_IT + 2 * ns];
+          itnB = lf[F_IT + 2 * ns + 1];
+        } else if (b == 1) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) hT1[h][jj] = relu(fmaf(rx0[h][jj], w1a, b1tB));
+        } else if (b >= 2 && b < 6) {
+          // g (x) H1 of K-step 1, two values per slot
+          const int h = (b - 2) >> 1, j0 = 2 * ((b - 2) & 1);
+#pragma unroll
+          for (int jj = j0; jj < j0 + 2; ++jj) {
+            __bf16 p0, p1, p2;
+            split3(hT1[h][jj] * rgg[h][jj], p0, p1, p2);
+            bq1[0][4 * h + jj] = p0;
+            bq1[1][4 * h + jj] = p1;
+            bq1[2][4 * h + jj] = p2;
+          }
+          if (b == 2) {
+            wa = lds4v(lf + F_W1T + fo);
+            xp0 = lds4v(lf + F_XP + ns * 64 + 4 * li);
+          } else if (b == 3) {
+            const bool ia = __builtin_amdgcn_readfirstlane(__float_as_int(itnA)) != 0;
+            const bool ib = __builtin_amdgcn_readfirstlane(__float_as_int(itnB)) != 0;
+            bbA = lds4v(lf + F_B1F + (ia ? 0 : kH) + fo);
+            bbB = lds4v(lf + F_B1F + (ib ? 0 : kH) + fo);
+          }
+        }
+        if (b >= 6 && b < 14) {
+          // layer 1 of group j+2, r-tile (b - 6) / 2: values, then the stores
+          const int rt = (b - 6) >> 1;
+          if (((b - 6) & 1) == 0) {
+            const f32x4 &bb = rt < 2 ? bbA : bbB;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) t1[jj] = relu(fmaf(xp0[rt], wa[jj], bb[jj]));
+          } else {
+            store_h1(t1, stb, rt);
+          }
+        }
+        if (b >= 4 && b < 12) {
+          // dW1 of the previous r-tile (two values per slot), the next rows
+          const int rt = (b - 4) >> 1, s = (b - 4) & 1;
+          if (rt > 0) {
+            dw1(2 * s, rt - 1);
+            dw1(2 * s + 1, rt - 1);
+          }
+          if (s == 1) {
+            const int r0 = 16 * rt + 4 * G;
+            dx0 = lds4v(xim + r0);
+            dgg = lds4v(gw + r0);
+          }
+        } else if (b == 12 || b == 13) {
+          dw1(2 * (b - 12), 3);
+          dw1(2 * (b - 12) + 1, 3);
+        }
+      };
+      bf16x8 A_c, A_n;
+      load_ops(0, A_c);
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        if (b + 1 < 16) load_ops(b + 1, A_n);
+        FENCE();
+        if (b < 4 || b >= 12) {
+          const int ot = b & 3;
+          const bf16x8(&bq)[3] = b < 4 ? bq0 : bq1;
+          accW2[ot] = mfma16(A_c, bq[2], accW2[ot]);
+          accW2[ot] = mfma16(A_c, bq[1], accW2[ot]);
+          accW2[ot] = mfma16(A_c, bq[0], accW2[ot]);
+        } else {
+          const int rt = (b - 4) >> 1, s = (b - 4) & 1, q = rt & 1;
+          if (s == 0) dh[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          const f16x8 Ah = __builtin_bit_cast(f16x8, A_c);
+          dh[q] = mfma16h(Ah, wd[s][1], dh[q]);
+          dh[q] = mfma16h(Ah, wd[s][0], dh[q]);
+        }
+        FENCE();
+        ytask(b);
+        FENCE();
+        A_c = A_n;
+      }
+      if (iaA)
+        sa += sgA;
+      else
+        sb += sgA;
+      if (iaB)
+        sa += sgB;
+      else
+        sb += sgB;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];
+  }
+
+  // ---------------------------------------------------- slab write-out ----
+  float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
+  const float *w3g = P + PL.ow3();
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = 16 * ot + 4 * G + j;
+      slab[PL.oW2() + o * kH + 16 * w + li] = accW2[ot][j] * w3g[o];
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s3 = seg_sum<16>(accW3[j]);
+    const float s2 = seg_sum<16>(accB2[j]);
+    const int o = 16 * w + 4 * G + j;
+    if (li == 0) {
+      slab[PL.ow3() + o] = s3 * (1.0f / S2);
+      slab[PL.ob2() + o] = s2 * w3g[o];
+    }
+  }
+  if (w == 0) {
+    const float v3 = seg_sum<64>(accB3);
+    if (l == 0) slab[PL.ob3()] = v3;
+  }
+  {
+    float tw0 = w0 + __shfl_xor(w0, 16, kWave);
+    float va = sa + __shfl_xor(sa, 16, kWave);
+    float vb = sb + __shfl_xor(sb, 16, kWave);
+    tw0 += __shfl_xor(tw0, 32, kWave);
+    va += __shfl_xor(va, 32, kWave);
+    vb += __shfl_xor(vb, 32, kWave);
+    // dH1 was in units of S_D
+    tw0 *= 1.0f / SD;
+    va *= 1.0f / SD;
+    vb *= 1.0f / SD;
+    if (G == 0) {
+      const int i = 16 * w + li;
+      slab[PL.oW1() + i * kF0 + 0] = tw0;
+      slab[PL.oW1() + i * kF0 + kD] = va * ((float)a.env.item_a[0] / (float)kCapacity) +
+                                      vb * ((float)a.env.item_b[0] / (float)kCapacity);
+      slab[PL.ob1() + i] = va + vb;
+    }
+  }
+}
+#undef FENCE
+
+}  // namespace s4h
+
+hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)s4h::policy_train_split4h_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s4h::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(s4h::policy_train_split4h_kernel, dim3(grid),
+                     dim3(s4h::kThreads), s4h::kLds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace xh

@@ -540,7 +540,8 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 // (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel; for
 // the 128-bin 3-D shape the default is the pipelined 8-wave kernel
 // (policy_split8x_kernels.hip) and =split128 keeps the 4-wave one
-// (policy_split128_kernels.hip).
+// (policy_split128_kernels.hip); the 32-bin 1-D [64,64] shape runs the
+// pipelined 4-wave kernel on f16 pairs (policy_split4h_kernels.hip).
 // Diagnostic overrides, read per launch and reported by
 // xh_trainer_kernel_info.
 bool train_split_enabled() {
@@ -554,6 +555,8 @@ static bool train_kernel_is(const char *name) {
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
   const bool algo = a.algo == kPPO || a.algo == kAC;
+  if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
+    return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
   return algo && H1 == 128 && H2 == 128 &&
          ((a.env.B == split::kB && a.env.D == split::kD) ||
           (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims));
@@ -562,6 +565,13 @@ bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
 hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
                                      hipStream_t s, KernelInfo *info) {
   if (info) info->math = kMathSplitTrain;
+  if (a.env.B == kSplit4hBins) {
+    if (info) {
+      info->name = "policy_train_split4h_kernel";
+      info->math = kMathSplitTrainF16;
+    }
+    return launch_policy_train_split4h(a, grid, s);
+  }
   if (a.env.B == kSplit128Bins) {
     if (info) info->math = kMathSplitTrainF16;
     if (!train_kernel_is("split128")) {

@@ -301,10 +301,11 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
 hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                int grid, hipStream_t s,
                                KernelInfo *info = nullptr);
-// The f32-accurate bf16-split train kernels for the 64-bin 2-D
-// (policy_split_kernels.hip) and 128-bin 3-D (policy_split128_kernels.hip)
-// [128,128] shapes; XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.
+// The f32-accurate split train kernels for the 64-bin 2-D and 128-bin 3-D
+// [128,128] shapes and the 32-bin 1-D [64,64] one (dispatch in
+// policy_split_kernels.hip); XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.
 constexpr int kSplit128Bins = 128, kSplit128Dims = 3;
+constexpr int kSplit4hBins = 32;
 bool train_split_enabled();
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2);
 hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
@@ -319,6 +320,8 @@ hipError_t launch_policy_train_split4p(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
+hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
 hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);

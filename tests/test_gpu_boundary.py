@@ -95,12 +95,16 @@ def test_env_overrides_of_many_envs(ctx):
     tr.close()
 
 
-@pytest.mark.parametrize("B,D,widths,train,roll,prod", [
-    (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 8.0 / 3.0),
-    (8, 2, (128, 64), None, None, None),
+@pytest.mark.parametrize("B,D,widths,train,roll,prod,f32_train", [
+    (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 8.0 / 3.0,
+     "policy_train8_kernel"),
+    # config 2's shape: the split train kernel, the f32 rollout
+    (32, 1, (64, 64), "policy_train_split4h_kernel", "rollout_step_kernel", 8.0 / 3.0,
+     "policy_train_kernel"),
+    (8, 2, (128, 64), None, None, None, None),
 ])
 def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
-                                    prod):
+                                    prod, f32_train):
     """xh_trainer_kernel_info reports the kernels the last rollout step and
     policy epoch launched, their arithmetic and its MFMA peak; an override
     variable shows up in the report and changes what runs."""
@@ -118,8 +122,11 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
         assert kt["math"] == "f16_pair_bf16_split"
         assert kt["products_per_f32_product"] == pytest.approx(prod, rel=1e-5)
         assert kt["peak_tflops"] == pytest.approx(2500.0 / prod, rel=1e-5)
-        assert kr["math"] == "f16_pair"
-        assert kr["peak_tflops"] == pytest.approx(2500.0 / 3)
+        if roll.startswith("rollout_split"):
+            assert kr["math"] == "f16_pair"
+            assert kr["peak_tflops"] == pytest.approx(2500.0 / 3)
+        else:
+            assert kr["math"] == "f32_mfma"
     else:
         assert kt["math"] == "f32_mfma" and kt["peak_tflops"] == 157.3
         assert kt["kernel"].startswith("policy_train")
@@ -133,5 +140,5 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
         k = tr.kernel_info()
         assert k["overrides"]["XH_TRAIN_KERNEL"] == "f32"
         assert k["policy_train"]["math"] == "f32_mfma"
-        assert k["policy_train"]["kernel"] == "policy_train8_kernel"
+        assert k["policy_train"]["kernel"] == f32_train
         tr.close()

@@ -331,22 +331,23 @@ def test_c3_reference_lr_on_row_sums_diverges(ctx):
     assert first is not None
 
 
-@pytest.mark.parametrize("algo,B,D,N,T", [("ppo", 64, 2, 160, 4),
-                                         ("ac", 128, 3, 24, 8)])
-def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T):
-    """The config-3 and config-5 train kernels run their three 128x128 GEMMs
-    as six bf16 MFMAs per K-slice on exactly split f32 operands
-    (csrc/xh_split.h).  Its
-    policy gradients stay within the stated row-summed bound and within a
-    small factor of the f32-MFMA kernel's distance to the oracle's
-    double-precision sums on the same batch (640 row groups, several per
-    workgroup), error per entry in units of u * sum|terms| (measured: max
-    435 vs 272, median 0.37 vs 0.18 -- both under one rounding unit of the
-    terms' magnitude, against a bound of n + 8 = 40968 units)."""
+@pytest.mark.parametrize("algo,B,D,N,T,widths", [("ppo", 64, 2, 160, 4, (128, 128)),
+                                                ("ac", 128, 3, 24, 8, (128, 128)),
+                                                ("ppo", 32, 1, 768, 4, (64, 64))])
+def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T, widths):
+    """The config-3, config-5 and config-2 train kernels run their GEMMs on
+    exactly split operands (f16 pairs for layer 2 and dH1, the three-part
+    bf16 split for dW2; csrc/xh_split.h).  Their policy gradients stay
+    within the stated row-summed bound and within a small factor of the
+    f32-MFMA kernel's distance to the oracle's double-precision sums on the
+    same batch (several row groups per workgroup), error per entry in units
+    of u * sum|terms| (round 2, config 3: max 435 vs 272, median 0.37 vs 0.18
+    -- both under one rounding unit of the terms' magnitude, against a bound
+    of n + 8 = 40968 units)."""
     from oracle import pyoracle as po
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import BUF_POLICY_GRADS
-    widths, x0 = (128, 128), 24681357
+    x0 = 24681357
     pp = init_policy(D, *widths, seed=11)
     vp = init_value(B, D, seed=12)
     orc = _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo)
