@@ -490,9 +490,12 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
         unsigned m[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
-        const u32x2 mm = {m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
-        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm * 0x3F80u));
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm * 0x3C00u));
+        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
+        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
+        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
+                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
+        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
+        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
       } else if (k == 20) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 22) {
