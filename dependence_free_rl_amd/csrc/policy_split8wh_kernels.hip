@@ -92,6 +92,21 @@
   } while (0)
 #endif
 
+// XH_TRACE_X=1 (diagnostic trace builds only): the stamps 1-7 inside X
+// instead (after tasks 15, 31, 43, 45, layer 2's end, the partial logits,
+// the barrier)
+#ifndef XH_TRACE_X
+#define XH_TRACE_X 0
+#endif
+#define S8H_STAMP_Y(a, gi, w, lane, slot) \
+  do {                                    \
+    if (!XH_TRACE_X) S8H_STAMP(a, gi, w, lane, slot); \
+  } while (0)
+#define S8H_STAMP_X(a, gi, w, lane, slot) \
+  do {                                    \
+    if (XH_TRACE_X) S8H_STAMP(a, gi, w, lane, slot); \
+  } while (0)
+
 namespace xh {
 namespace s8h {
 
@@ -385,11 +400,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
         *reinterpret_cast<const unsigned short *>(a.b.bins + ti * (kB * kD) + lo);
     // one branch-free load per lane (lanes 3.. the item's first two
     // coordinates), so nothing waits for it before its use
-    const int *src = l == 0   ? a.b.action + ti
-                     : l == 1 ? reinterpret_cast<const int *>(a.b.pold + ti)
-                     : l == 2 ? reinterpret_cast<const int *>(a.adv + ti)
-                              : reinterpret_cast<const int *>(a.b.items + ti * 4);
-    return Raw{bins, *src};
+    // (the address chosen by selects, not branches)
+    const unsigned long long p0 = (unsigned long long)(a.b.action + ti);
+    const unsigned long long p1 = (unsigned long long)(a.b.pold + ti);
+    const unsigned long long p2 = (unsigned long long)(a.adv + ti);
+    const unsigned long long p3 = (unsigned long long)(a.b.items + ti * 4);
+    unsigned long long pa = l >= 3 ? p3 : p2;
+    pa = l == 1 ? p1 : pa;
+    pa = l == 0 ? p0 : pa;
+    return Raw{bins, *reinterpret_cast<const int *>(pa)};
   };
   auto stage_store = [&](const Raw &r, int s) {
     const float x0 = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
@@ -488,7 +507,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   // ---- pipeline prologue: groups 0 and 1 staged (group 2's rows loaded),
   // layer 1 and layer 2 of group 0 (its partial logits), layer 1 of group 1
   f32x4 pre_cur[4];
-  Raw raw = {0, 0};
   if (w == 0) {
     stage_store(stage_load(0), 0);
     stage_store(stage_load(1), 1);
@@ -507,6 +525,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     int rdb = rdb0, trm0 = trm00, trm1 = trm10, stb = stb0;
     asm volatile("" : "+v"(rdb), "+v"(trm0), "+v"(trm1), "+v"(stb), "+s"(gstep));
     S8H_STAMP(a, j, w, l, 0);
+    // (defined and used under w == 0 only: no value flows round the loop,
+    // so nothing waits for the loads before the stores)
+    Raw raw;
     if (w == 0) raw = stage_load(j + 2);
     const float *xim = lf + F_X + cs * 128;
     // T-layout constants of feature 16w + li (re-read: cheaper than holding)
@@ -528,6 +549,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     float b1t = 0.0f;
     f32x4 w3;
     auto xtask = [&](int k) {
+      if (k == 16) S8H_STAMP_X(a, j, w, l, 1);
+      if (k == 32) S8H_STAMP_X(a, j, w, l, 2);
+      if (k == 44) S8H_STAMP_X(a, j, w, l, 3);
+      if (k == 46) S8H_STAMP_X(a, j, w, l, 4);
       if (k == 0) {
         const float zs = ((z0[0] + z0[1]) + (z0[2] + z0[3])) +
                          ((z1[0] + z1[1]) + (z1[2] + z1[3]));
@@ -641,11 +666,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     };
     f32x4 pre_nx[4];
     layer2(rdb, pre_nx, xtask);
-    S8H_STAMP(a, j, w, l, 1);
+    S8H_STAMP_Y(a, j, w, l, 1);
+    S8H_STAMP_X(a, j, w, l, 5);
     partials(pre_nx, w3, (j + 1) & 1);
-    S8H_STAMP(a, j, w, l, 2);
+    S8H_STAMP_Y(a, j, w, l, 2);
+    S8H_STAMP_X(a, j, w, l, 6);
     __syncthreads();
-    S8H_STAMP(a, j, w, l, 3);
+    S8H_STAMP_Y(a, j, w, l, 3);
+    S8H_STAMP_X(a, j, w, l, 7);
 
     // ================= Y(j): dW2 / dH1 of group j with VALU of j, j+2 =====
     // 32 blocks: b < 16 dW2, three bf16 MFMAs (ks = b / 8, ot = b % 8: dW2 +=
@@ -772,18 +800,18 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
         FENCE();
         A_c = A_n;
       }
-      S8H_STAMP(a, j, w, l, 4);
+      S8H_STAMP_Y(a, j, w, l, 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s) dw1(s, 3);
       if (item_cur)
         sa += sg;
       else
         sb += sg;
-      S8H_STAMP(a, j, w, l, 5);
+      S8H_STAMP_Y(a, j, w, l, 5);
     }
     __syncthreads();
-    S8H_STAMP(a, j, w, l, 6);
-    S8H_STAMP(a, j, w, l, 7);
+    S8H_STAMP_Y(a, j, w, l, 6);
+    S8H_STAMP_Y(a, j, w, l, 7);
     // rotate the pipeline
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];
