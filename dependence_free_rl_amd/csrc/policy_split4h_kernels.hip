@@ -169,10 +169,21 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   // the W2 / W2' fragments of tile w as f16 pairs
   {
     float mw = 0.0f, md = 0.0f, mh = 0.0f;
-    for (int e = tid; e < kH * kH; e += kThreads) {
-      const float v = P[PL.oW2() + e];
-      mw = fmaxf(mw, fabsf(v));
-      md = fmaxf(md, fabsf(v * P[PL.ow3() + e / kH]));
+    {
+      // thread t: row t / 4 of W2, its quarter t % 4 (four 16-byte loads)
+      const int o = tid >> 2;
+      const float4 *src = reinterpret_cast<const float4 *>(P + PL.oW2() + o * kH + 16 * (tid & 3));
+      const float w3o = P[PL.ow3() + o];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v4 = src[q];
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          mw = fmaxf(mw, fabsf(v[u]));
+          md = fmaxf(md, fabsf(v[u] * w3o));
+        }
+      }
     }
     if (tid < kH) {
       const float wv = P[PL.oW1() + tid * kF0 + kD];

@@ -28,8 +28,8 @@ def _oracle_trainer(B, D, N, T, widths, pp, vp, x0, algo):
     # config 2 shape, 1536 two-env groups: 3 per train workgroup (2 x 256)
     ("ppo", 32, 1, (64, 64), 768, 4),
     ("ac", 32, 1, (64, 64), 96, 4),      # AC through the config-2 split kernel
-    # an odd number of transitions: the config-2 shape's f32 fallback
-    ("ppo", 32, 1, (64, 64), 9, 3),
+    # an odd number of two-env groups (15)
+    ("ppo", 32, 1, (64, 64), 10, 3),
     ("ac", 16, 2, (64, 64), 64, 8),
     ("ac", 128, 3, (128, 128), 8, 8),    # config 5 shape
     # config 5 shape, 768 row groups: 3 per train workgroup (256)
