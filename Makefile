@@ -17,6 +17,7 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/policy_split4p_kernels.o $(SRC)/policy_split8wh_kernels.o \
             $(SRC)/policy_split8x_kernels.o \
             $(SRC)/policy_split4h_kernels.o \
+            $(SRC)/policy_split8wg_kernels.o \
             $(SRC)/xylo_hip.o
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h include/xylo_hip.h
 
@@ -51,6 +52,7 @@ FLAGS_policy_split4p_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split8wh_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split8x_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split4h_kernels := -mllvm -amdgpu-mfma-vgpr-form
+FLAGS_policy_split8wg_kernels := -mllvm -amdgpu-mfma-vgpr-form
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@

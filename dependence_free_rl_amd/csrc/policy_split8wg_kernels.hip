@@ -1,68 +1,23 @@
-// policy_split8wh_kernels.hip -- the PPO / actor-critic train epoch of the
+// policy_split8wg_kernels.hip -- the PPO / actor-critic train epoch of the
 // 64-bin 2-D [128,128] policy (BASELINE configs 3 and 4): the pipelined
-// 8-wave kernel of policy_split8wp_kernels.hip with layer 2 and dH1 on the
-// f16 matrix cores, each f32 operand scaled by a power of two and split
-// EXACTLY into two f16 parts ("f16 pairs"):
+// 8-wave f16-pair kernel of policy_split8wh_kernels.hip (see its header: f16
+// pairs, pipeline, layouts) with dW2 on f16 pairs as well, taking both of its
+// operands from LDS images instead of building them in registers:
 //
-//     S x = hi + lo + e,  hi = f16(S x), lo = f16(S x - hi),  |e| <= 2^-22 |S x|
+//     dW2 = M^T (g (x) H1) = (M o g)^T H1
 //
-// (11 significant bits per part, round to nearest; S x - hi is exact).  The
-// scales are per launch, chosen from the operands' maxima so that |S x| <=
-// 2^14 (f16's range ends at 65504): W2 and W2' = diag(w3) W2 from the
-// parameters, H1 from the bound |H1[r][i]| <= |W1[i][0]| + |W1[i][1]| +
-// |b1_item[i]| (|bins / 8| <= 1).  A product of two f16 values is exact in
-// f32, so a dot product is
+// B = H1 itself, the f16-pair H1 image of the group (three images, one per
+// pipeline slot, so the group's H1 is still there in Y(j)); A = the relu mask
+// weighted by the row's loss gradient, g S_g M, as an f16-pair image (hi and
+// lo), written in X(j) where the plain 0/1 mask image used to be.  S_g is a
+// per-group power of two (|g S_g| < 2^14 from the group's max |g|, the
+// exponent rounded up to a multiple of 4 so that consecutive groups mostly
+// share it); the dW2 accumulators are kept in units of the current group's
+// S_g S_H and rescaled by an exact power of two when it changes.  Per wave
+// per group this drops the recomputed H1 values (T layout) and the
+// three-part bf16 split of g (x) H1 (about 170 VALU) for a second mask image
+// and three f16 MFMAs per dW2 block instead of three bf16 ones.
 //
-//     (S_a a).(S_b b) = hi.hi + hi.lo + lo.hi + d,  |d| <= 3 2^-22 sum|a_k b_k|
-//
-// (the dropped lo.lo and the two e terms): three MFMAs per K = 32 slice for
-// layer 2 instead of the bf16 split's six, and two for dH1 (its mask operand
-// is exact in f16) instead of three.  Results stay in scaled units where
-// only signs matter (the relu masks) and are unscaled exactly (powers of two)
-// in the partial logits (w3 / (S_W S_H)), in dW3 and in dW1 at the write-out.
-// dW2's operand g (x) H1 has no bound known before the kernel (g ~ A / p_old),
-// so dW2 keeps the exact three-part bf16 split.  MFMAs per wave per 64-row
-// group: 192 -> 128.  Pipeline, layouts and swizzles as in
-// policy_split8wp_kernels.hip:
-//
-// Why: the two waves of a SIMD run the same phases in lockstep, so a VALU
-// block and an MFMA block do not overlap, while VALU instructions issued
-// between one wave's own MFMAs are nearly free (tools/probes/
-// interleave_probe.hip: 96 v_mfma_f32_16x16x32_bf16 per wave at two waves
-// per SIMD take 3083 cycles alone, 3200 with two independent v_fma_f32 after
-// each MFMA, 4025 with the same VALU as a block after them).  A group's
-// softmax, loss gradient, masks, dW3 / db2 sums, g (x) H1 splits, dW1 sums
-// and layer 1 have no MFMA work of their own group to hide under, so the
-// loop runs two groups at once:
-//
-//   X(j): MFMA  layer 2 of group j+1 (96 per wave)
-//         VALU  softmax + loss gradient of group j, its relu masks (image),
-//               dW3 / db2 sums, the first K-step's g (x) H1 fragments;
-//               then group j+1's partial logits      -> barrier
-//   Y(j): MFMA  dW2 and dH1 of group j (96 per wave)
-//         VALU  the second K-step's g (x) H1 fragments, layer 1 of group
-//               j+2 (-> H1 image), dW1 / db1 / item sums of group j
-//                                                     -> barrier
-//
-// Waves issue in order, so a task must never wait: the VALU work is cut into
-// slots of independent instructions after each block of three MFMAs
-// (sched_barrier-fenced), and every LDS value a slot uses was loaded at
-// least one slot earlier and before the next block's operand prefetch (LDS
-// returns in order, so a consumer then waits for nothing younger).  The
-// partial logits are summed over lane groups with v_permlane16/32_swap (no
-// LDS round trip); each wave keeps its own copies of the rows' loss
-// gradients, in row order and in the C layout's order, so no barrier
-// separates producing and using them; the X rows are staged in both orders.
-// Image addresses are plain integers (dynamic LDS starts at 0: this kernel
-// has no static LDS) so the region and tile offsets fold into the ds_read /
-// ds_write immediates.
-//
-// Layouts, swizzle and operand maps: "C layout" = the 16x16 MFMA result,
-// lane column li = l & 15 (a row of the group), registers rows 4G + j (G =
-// l >> 4; features); "T layout" = lane feature, registers rows.  Images are
-// [64 rows][128 x bf16] with 16-byte chunks XOR-swizzled by swz2(row & 15)
-// (conflict-free for the 16x16x32 row reads in the natural chunk order 4s +
-// G, for ds_read_b64_tr_b16 and for the C-layout ds_write_b64 stores).
 #include <cstdlib>
 
 #include "xh_device.h"
@@ -79,7 +34,7 @@
 #define XH_DIAG_TRACE 0
 #endif
 #if XH_DIAG_TRACE
-#define S8H_STAMP(a, gi, w, lane, slot)                                         \
+#define S8G_STAMP(a, gi, w, lane, slot)                                         \
   do {                                                                        \
     if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups &&      \
         (lane) == 0)                                                          \
@@ -87,7 +42,7 @@
                 (slot)] = clock64();                                          \
   } while (0)
 #else
-#define S8H_STAMP(a, gi, w, lane, slot) \
+#define S8G_STAMP(a, gi, w, lane, slot) \
   do {                                  \
   } while (0)
 #endif
@@ -98,33 +53,29 @@
 #ifndef XH_TRACE_X
 #define XH_TRACE_X 0
 #endif
-#define S8H_STAMP_Y(a, gi, w, lane, slot) \
+#define S8G_STAMP_Y(a, gi, w, lane, slot) \
   do {                                    \
-    if (!XH_TRACE_X) S8H_STAMP(a, gi, w, lane, slot); \
+    if (!XH_TRACE_X) S8G_STAMP(a, gi, w, lane, slot); \
   } while (0)
-#define S8H_STAMP_X(a, gi, w, lane, slot) \
+#define S8G_STAMP_X(a, gi, w, lane, slot) \
   do {                                    \
-    if (XH_TRACE_X) S8H_STAMP(a, gi, w, lane, slot); \
+    if (XH_TRACE_X) S8G_STAMP(a, gi, w, lane, slot); \
   } while (0)
 
 namespace xh {
-namespace s8h {
+namespace s8g {
 
 constexpr int kB = 64, kD = 2, kF0 = 2 * kD, kH = 128;
-// relu masks from the pre-activations' bits (relu_bit): 2.37 -> 2.28 ms per
-// epoch against compare + select (the VCC hazard's s_nops)
-#ifndef XH_8WH_IMASK
-#define XH_8WH_IMASK 1
-#endif
 constexpr int kThreads = 512;
 constexpr int kImg = 64 * kImgRow;  // one 64-row part image, 16 KB
 // LDS carve (bytes): the H1 image (two f16 parts, scaled by S_H), the mask
 // image as bf16 (dW2's A operand, transposed reads) and as f16 (dH1's A
 // operand, row reads), then f32.  W2 / W2' live in registers as f16 pairs.
-constexpr int L_H1 = 0;
-constexpr int L_MASK = 2 * kImg;
-constexpr int L_MASKH = 3 * kImg;
-constexpr int L_F = 4 * kImg;
+constexpr int L_H1 = 0;              // [3 slots][2 parts] H1 images (S_H)
+constexpr int kH1Slot = 2 * kImg;    // bytes per slot
+constexpr int L_GM = 6 * kImg;       // [2 parts] g S_g M (dW2's A operand)
+constexpr int L_MASKH = 8 * kImg;    // f16 0/1 mask (dH1's A operand)
+constexpr int L_F = 9 * kImg;
 constexpr int F_W1T = 0;               // [2 k][128 i]: W1[i][k], the bin columns
 constexpr int F_B1F = F_W1T + 2 * kH;  // [2 items][128]: b1 + the item's part
 constexpr int F_B2 = F_B1F + 2 * kH;   // [128]
@@ -214,17 +165,6 @@ __device__ __forceinline__ int trw_base(int l, int t) {
 __device__ __forceinline__ int st_base(int G, int li) {
   return kImgRow * li + 16 * ((G >> 1) ^ swz2(li)) + 8 * (G & 1);
 }
-__device__ __forceinline__ void split4(const f32x4 &v, bf16x4 &ph, bf16x4 &pm,
-                                       bf16x4 &pl) {
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    __bf16 a, b, c;
-    split3(v[u], a, b, c);
-    ph[u] = a;
-    pm[u] = b;
-    pl[u] = c;
-  }
-}
 __device__ __forceinline__ f32x4 lds4v(const float *p) {
   return *reinterpret_cast<const f32x4 *>(p);
 }
@@ -250,7 +190,7 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
-__global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
+__global__ __launch_bounds__(kThreads, 2) void policy_train_split8wg_kernel(
     PolicyTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
@@ -369,8 +309,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   }
   // per-lane absolute LDS bases (the region offsets that exceed the 16-bit
   // immediate folded in)
-  const int trm00 = trm_base(l, 0), trm10 = trm_base(l, 1);  // ^ 32 ot, + L_MASK
-  const int stb0 = st_base(G, li) ^ (32 * w);  // + L_H1 / L_MASK + 4096 rt
+  const int trm00 = trm_base(l, 0), trm10 = trm_base(l, 1);  // ^ 32 ot, + L_GM / L_H1
+  const int stb0 = st_base(G, li) ^ (32 * w);  // + L_H1 / L_GM / L_MASKH + 4096 rt
   const int fo = 16 * w + 4 * G;  // this lane's 4 features in the C layout
   float *gw = lf + F_GW + 64 * w;  // this wave's copies of the rows' g
   float *gp = lf + F_GP + 64 * w;
@@ -437,7 +377,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     st4h(sb + L_H1 + 4096 * rt, ph);
     st4h(sb + L_H1 + kImg + 4096 * rt, pl);
   };
-  // layer 1 (C layout) of the group in slot s, all four r-tiles -> H1 image
+  // layer 1 (C layout) of the group in slot s, all four r-tiles -> its H1
+  // image (stb: the store base with the slot's offset folded in)
   auto layer1_all = [&](int s, int stb) {
     const bool ia = lf[F_IT + s] != 0.0f;
     const f32x4 wa = lds4v(lf + F_W1T + fo), wb = lds4v(lf + F_W1T + kH + fo);
@@ -517,14 +458,27 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   layer2(rdb0, pre_cur, no_task);
   partials(pre_cur, lds4v(lf + F_W3 + fo), 0);
   __syncthreads();
-  layer1_all(1, stb0);
+  layer1_all(1, stb0 + kH1Slot);
   __syncthreads();
 
+  // dW2's accumulators are in units of 2^(14 - erun) S_H
+  int erun = 0;
   for (int j = 0; j < J; ++j) {
     const int cs = j % 3, ns = (j + 2) % 3;  // slots of groups j and j + 2
-    int rdb = rdb0, trm0 = trm00, trm1 = trm10, stb = stb0;
-    asm volatile("" : "+v"(rdb), "+v"(trm0), "+v"(trm1), "+v"(stb), "+s"(gstep));
-    S8H_STAMP(a, j, w, l, 0);
+    // H1 slots: group j+1's (layer 2 in X), group j's (dW2 in Y), group
+    // j+2's (layer 1 in Y)
+    const int h1n = ((j + 1) % 3) * kH1Slot, h1c = cs * kH1Slot, h1s = ns * kH1Slot;
+    // per-lane absolute bases with the regions past the 16-bit ds offset
+    // field folded in (the XOR'd bits 5-7 do not meet the region bits, so
+    // (base + region) ^ x = (base ^ x) + region): rdb H1 slot j+1 rows; trg
+    // dW2's A (g S_g M); trh dW2's B (H1 slot j, tile w); stg the mask
+    // stores; sth the layer-1 stores (slot j+2); rdm dH1's A (0/1 mask)
+    int rdb = rdb0 + h1n, trg0 = trm00 + L_GM, trg1 = trm10 + L_GM;
+    int trh0 = (trm00 ^ (32 * w)) + L_H1 + h1c, trh1 = (trm10 ^ (32 * w)) + L_H1 + h1c;
+    int stg = stb0 + L_GM, sth = stb0 + L_H1 + h1s, rdm = rdb0 + L_MASKH;
+    asm volatile("" : "+v"(rdb), "+v"(trg0), "+v"(trg1), "+v"(stg), "+s"(gstep));
+    asm volatile("" : "+v"(trh0), "+v"(trh1), "+v"(sth), "+v"(rdm));
+    S8G_STAMP(a, j, w, l, 0);
     // (defined and used under w == 0 only: no value flows round the loop,
     // so nothing waits for the loads before the stores)
     Raw raw;
@@ -541,18 +495,21 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     const float b3 = lf[F_B3];
     const f32x4 rec = lds4v(lf + F_REC + 4 * cs);
     const float itc = lf[F_IT + cs];
-    f32x4 gx0[2], gx1[2];
     float ex = 0.0f, se = 0.0f, gz = 0.0f;
-    f32x4 gr4, ggk[2], hT[2];
-    bf16x8 bq0[3];
+    f32x4 gr4;
+    // the group's dW2 scale S_g = 2^(14 - eg) (eg: max |g| < 2^eg, rounded up
+    // to a multiple of 4) and g S_g of the lane's four C-layout rows as f16
+    // pair bits
+    int eg = 0;
+    unsigned gh[4], gl[4];
     bool item_cur = false;
     float b1t = 0.0f;
     f32x4 w3;
     auto xtask = [&](int k) {
-      if (k == 16) S8H_STAMP_X(a, j, w, l, 1);
-      if (k == 32) S8H_STAMP_X(a, j, w, l, 2);
-      if (k == 44) S8H_STAMP_X(a, j, w, l, 3);
-      if (k == 46) S8H_STAMP_X(a, j, w, l, 4);
+      if (k == 16) S8G_STAMP_X(a, j, w, l, 1);
+      if (k == 32) S8G_STAMP_X(a, j, w, l, 2);
+      if (k == 44) S8G_STAMP_X(a, j, w, l, 3);
+      if (k == 46) S8G_STAMP_X(a, j, w, l, 4);
       if (k == 0) {
         const float zs = ((z0[0] + z0[1]) + (z0[2] + z0[3])) +
                          ((z1[0] + z1[1]) + (z1[2] + z1[3]));
@@ -586,22 +543,25 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
         accB3 += gz;  // wave 0's is written out
         item_cur = __builtin_amdgcn_readfirstlane(__float_as_int(itc)) != 0;
         b1t = lf[F_B1F + (item_cur ? 0 : kH) + 16 * w + li];
-        // the rows of K-step 0 (T layout)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          gx0[h] = lds4v(xim + 16 * h + 4 * G);
-          gx1[h] = lds4v(xim + 64 + 16 * h + 4 * G);
-        }
+      } else if (k == 4) {
+        // max |g| over the group's 64 rows (every wave holds all of g; the
+        // order of the magnitude bits is the order of the floats)
+        unsigned gb = __float_as_uint(gz) & 0x7FFFFFFFu;
+        gb = max(gb, (unsigned)__builtin_amdgcn_mov_dpp((int)gb, 0xB1, 0xF, 0xF, false));
+        gb = max(gb, (unsigned)__builtin_amdgcn_mov_dpp((int)gb, 0x4E, 0xF, 0xF, false));
+        gb = max(gb, (unsigned)__builtin_amdgcn_mov_dpp((int)gb, 0x141, 0xF, 0xF, false));
+        gb = max(gb, (unsigned)__builtin_amdgcn_mov_dpp((int)gb, 0x140, 0xF, 0xF, false));
+        const unsigned gm =
+            max(max((unsigned)__builtin_amdgcn_readlane((int)gb, 0),
+                    (unsigned)__builtin_amdgcn_readlane((int)gb, 16)),
+                max((unsigned)__builtin_amdgcn_readlane((int)gb, 32),
+                    (unsigned)__builtin_amdgcn_readlane((int)gb, 48)));
+        // frexp exponent of max |g| (max |g| < 2^e), up to a multiple of 4,
+        // within [-40, 40]
+        const int e = (int)((gm >> 23) & 0xFFu) - 126;
+        eg = min(max((e + 3) & ~3, -40), 40);
       } else if (k == 5) {
         gr4 = lds4v(gp + 4 * li);  // g of rows 16 rt + li
-#pragma unroll
-        for (int h = 0; h < 2; ++h) ggk[h] = lds4v(gw + 16 * h + 4 * G);
-      } else if (k == 7 || k == 8) {
-        // layer-1 values of K-step 0's rows (T layout), r-tile h
-        const int h = k - 7;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          hT[h][jj] = relu(fmaf(gx1[h][jj], w1b, fmaf(gx0[h][jj], w1a, b1t)));
       } else if (k >= 11 && k < 15) {
         // dW3 / db2 of r-tile rt (pre-activations in units of S2: dW3 is
         // unscaled at the write-out)
@@ -609,54 +569,39 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float v = pre_cur[rt][jj];
-#if XH_8WH_IMASK
           // relu'(v) as an integer clamp of v's bits (v_med3: no compare,
           // no VCC hazard)
           const float gm = gr4[rt] * (float)relu_bit(v);
-#else
-          const float gm = v > 0.0f ? gr4[rt] : 0.0f;
-#endif
           accW3[jj] = fmaf(gm, v, accW3[jj]);  // g relu(v)
           accB2[jj] += gm;                     // g M (w3 at the write-out)
         }
       } else if (k >= 16 && k < 20) {
-        // g (x) H1 of K-step 0, two values per slot
-        const int h = (k - 16) >> 1, j0 = 2 * ((k - 16) & 1);
-#pragma unroll
-        for (int jj = j0; jj < j0 + 2; ++jj) {
-          __bf16 p0, p1, p2;
-          split3(hT[h][jj] * ggk[h][jj], p0, p1, p2);
-          bq0[0][4 * h + jj] = p0;
-          bq0[1][4 * h + jj] = p1;
-          bq0[2][4 * h + jj] = p2;
-        }
+        // g S_g of row 16 rt + li as an f16 pair (the bits, zero-extended)
+        const int rt = k - 16;
+        _Float16 h0, h1;
+        split2h(gr4[rt] * __int_as_float((141 - eg) << 23), h0, h1);
+        gh[rt] = __builtin_bit_cast(unsigned short, h0);
+        gl[rt] = __builtin_bit_cast(unsigned short, h1);
       } else if (k >= 20 && k < 24) {
-        // the relu masks of r-tile k - 20 (C layout) -> the bf16 and f16
-        // mask images (1.0 = 0x3F80 / 0x3C00: the f16 bits are the bf16
-        // bits & 0x3C00)
+        // the relu masks of r-tile k - 20 (C layout) -> dW2's g S_g M images
+        // (hi, lo) and dH1's 0/1 image, all f16
         const int rt = k - 20;
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-#if XH_8WH_IMASK
-        // 0 / 1 per value from the bits, two per dword, times the 1.0 bits
+        // 0 / 1 per value from the bits, two per dword
         unsigned m[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
           m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
-        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
-        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
-        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
-                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
-        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
-#else
-        bf16x4 mk;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          mk[jj] = pre_cur[rt][jj] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
-        st4(stb + L_MASK + 4096 * rt, mk);
-        const u32x2 mb = __builtin_bit_cast(u32x2, mk) & 0x3C003C00u;
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mb));
-#endif
+        // times the f16 bits of g S_g's parts and of 1.0 by the full-rate
+        // 24-bit multiply (the 32-bit one is quarter rate)
+        const unsigned m01 = m[0] | (m[1] << 16), m23 = m[2] | (m[3] << 16);
+        const u32x2 mh = {(unsigned)__umul24(m01, gh[rt]), (unsigned)__umul24(m23, gh[rt])};
+        const u32x2 ml = {(unsigned)__umul24(m01, gl[rt]), (unsigned)__umul24(m23, gl[rt])};
+        const u32x2 m1 = {(unsigned)__umul24(m01, 0x3C00u), (unsigned)__umul24(m23, 0x3C00u)};
+        st4h(stg + 4096 * rt, __builtin_bit_cast(f16x4, mh));
+        st4h(stg + kImg + 4096 * rt, __builtin_bit_cast(f16x4, ml));
+        st4h(stg + (L_MASKH - L_GM) + 4096 * rt, __builtin_bit_cast(f16x4, m1));
+
       } else if (k == 36) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 44) {
@@ -666,52 +611,64 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     };
     f32x4 pre_nx[4];
     layer2(rdb, pre_nx, xtask);
-    S8H_STAMP_Y(a, j, w, l, 1);
-    S8H_STAMP_X(a, j, w, l, 5);
+    S8G_STAMP_Y(a, j, w, l, 1);
+    S8G_STAMP_X(a, j, w, l, 5);
     partials(pre_nx, w3, (j + 1) & 1);
-    S8H_STAMP_Y(a, j, w, l, 2);
-    S8H_STAMP_X(a, j, w, l, 6);
+    S8G_STAMP_Y(a, j, w, l, 2);
+    S8G_STAMP_X(a, j, w, l, 6);
     __syncthreads();
-    S8H_STAMP_Y(a, j, w, l, 3);
-    S8H_STAMP_X(a, j, w, l, 7);
+    S8G_STAMP_Y(a, j, w, l, 3);
+    S8G_STAMP_X(a, j, w, l, 7);
 
     // ================= Y(j): dW2 / dH1 of group j with VALU of j, j+2 =====
-    // 32 blocks, alternating: even b dW2 block d = b / 2, three bf16 MFMAs
-    // (ks = d / 8, ot = d % 8: dW2 += M^T (g (x) H1)), odd b dH1 block h =
-    // b / 2, two f16 MFMAs (rt = h / 4, s = h % 4: S_D dH1 = M (S_D W2'), the
-    // f16 mask image); operands one block ahead.  Alternating the two kinds
-    // spreads their LDS reads and the layer-1 / dW1 VALU evenly over the
-    // phase: 2.28 -> 2.21 ms per epoch against dW2 then dH1
+    // 32 blocks: b < 16 dW2, three f16 MFMAs (ks = b / 8, ot = b % 8: S_g S_H
+    // dW2 += (S_g g o M)^T (S_H H1), both from images), b >= 16 dH1, two f16
+    // MFMAs (rt = (b - 16) / 4, s = (b - 16) % 4: S_D dH1 = M (S_D W2'), the
+    // 0/1 image); A operands one block ahead
     {
+      // the accumulators into this group's units (exact powers of two)
+      if (eg != erun) {
+        const float r = __int_as_float((127 + erun - eg) << 23);
+#pragma unroll
+        for (int ot = 0; ot < 8; ++ot) accW2[ot] *= r;
+        erun = eg;
+      }
       float sg = 0.0f;
-      bf16x8 bq1[3];
-      f32x4 rx0[2], rx1[2], rgg[2], hT1[2];
       f32x4 wa, wb, bb, xp0, xp1, t1;
       float itn = 0.0f;
       f32x4 dx0, dx1, dgg;
       f32x4 dh[2];
-      // blocks alternate: even bb_ dW2 block bb_ / 2, odd bb_ dH1 block
-      // (bb_ - 1) / 2 (the two kinds' LDS reads and VALU interleaved)
-      auto load_ops = [&](int bb_, bf16x8 &A) {
-        const int b = bb_ >> 1;
+      struct AOp {
+        f16x8 h, l;
+      };
+      auto ldtrh = [&](int o0, int o1) { return __builtin_bit_cast(f16x8, ldtr(o0, o1)); };
+      // B: this group's H1 columns 16 w .. 16 w + 15 by transposed reads
+      f16x8 Bw[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          Bw[ks][p] = ldtrh(trh0 + p * kImg + 8192 * ks, trh1 + p * kImg + 8192 * ks);
+      // blocks alternate: even b dW2 block b / 2, odd b dH1 block (b - 1) / 2
+      // (the LDS reads of the two kinds interleaved)
+      auto load_ops = [&](int bb_, AOp &A) {
         if ((bb_ & 1) == 0) {
+          const int b = bb_ >> 1;
           const int ks = b >> 3, ot = b & 7;
-          A = ldtr((trm0 ^ (32 * ot)) + L_MASK + 8192 * ks,
-                   (trm1 ^ (32 * ot)) + L_MASK + 8192 * ks);
+          A.h = ldtrh((trg0 ^ (32 * ot)) + 8192 * ks, (trg1 ^ (32 * ot)) + 8192 * ks);
+          A.l = ldtrh((trg0 ^ (32 * ot)) + kImg + 8192 * ks,
+                      (trg1 ^ (32 * ot)) + kImg + 8192 * ks);
         } else {
+          const int b = bb_ >> 1;
           const int rt = b >> 2, s = b & 3;
-          A = ld8((rdb ^ (64 * s)) + L_MASKH + 4096 * rt);  // f16 bits
+          A.h = ld8h((rdm ^ (64 * s)) + 4096 * rt);
         }
       };
       // dW1 / db1 / item sums of value jj of r-tile rt (T layout)
       auto dw1 = [&](int jj, int rt) {
         const int q = rt & 1;
         const float tT = fmaf(dx1[jj], w1b, fmaf(dx0[jj], w1a, b1t));
-#if XH_8WH_IMASK >= 2
-        const float d = (dh[q][jj] * dgg[jj]) * (float)relu_bit(tT);
-#else
         const float d = tT > 0.0f ? dh[q][jj] * dgg[jj] : 0.0f;
-#endif
         sg += d;
         w0 = fmaf(d, dx0[jj], w0);
         w1 = fmaf(d, dx1[jj], w1);
@@ -729,46 +686,20 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
       };
       auto ytask = [&](int b) {
         if (b == 0) {
-          // rows of K-step 1 (T-layout r-tiles 2, 3) and their g; group
-          // j+2's item flag
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int r0 = 32 + 16 * h + 4 * G;
-            rx0[h] = lds4v(xim + r0);
-            rx1[h] = lds4v(xim + 64 + r0);
-            rgg[h] = lds4v(gw + r0);
-          }
-          itn = lf[F_IT + ns];
-        } else if (b == 2 || b == 3) {
-          const int h = b - 2;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            hT1[h][jj] = relu(fmaf(rx1[h][jj], w1b, fmaf(rx0[h][jj], w1a, b1t)));
-        } else if (b >= 4 && b < 8) {
-          // g (x) H1 of K-step 1, two values per slot
-          const int h = (b - 4) >> 1, j0 = 2 * ((b - 4) & 1);
-#pragma unroll
-          for (int jj = j0; jj < j0 + 2; ++jj) {
-            __bf16 p0, p1, p2;
-            split3(hT1[h][jj] * rgg[h][jj], p0, p1, p2);
-            bq1[0][4 * h + jj] = p0;
-            bq1[1][4 * h + jj] = p1;
-            bq1[2][4 * h + jj] = p2;
-          }
-          if (b == 4) {
-            // group j+2's layer-1 operands (C layout)
-            wa = lds4v(lf + F_W1T + fo);
-            wb = lds4v(lf + F_W1T + kH + fo);
-            xp0 = lds4v(lf + F_XP + ns * 128 + 4 * li);
-            xp1 = lds4v(lf + F_XP + ns * 128 + 64 + 4 * li);
-          } else if (b == 5) {
-            const bool ia = __builtin_amdgcn_readfirstlane(__float_as_int(itn)) != 0;
-            bb = lds4v(lf + F_B1F + (ia ? 0 : kH) + fo);
-          }
+          itn = lf[F_IT + ns];  // group j+2's item flag
+        } else if (b == 4) {
+          // group j+2's layer-1 operands (C layout)
+          wa = lds4v(lf + F_W1T + fo);
+          wb = lds4v(lf + F_W1T + kH + fo);
+          xp0 = lds4v(lf + F_XP + ns * 128 + 4 * li);
+          xp1 = lds4v(lf + F_XP + ns * 128 + 64 + 4 * li);
+        } else if (b == 5) {
+          const bool ia = __builtin_amdgcn_readfirstlane(__float_as_int(itn)) != 0;
+          bb = lds4v(lf + F_B1F + (ia ? 0 : kH) + fo);
         } else if ((b & 1) == 0 && b >= 8 && b < 24) {
           // layer 1 of group j+2 in the dW2 blocks' slots, r-tile (b - 8) /
-          // 4: values, then the split stores
-          layer1_rt((b - 8) >> 2, (b >> 1) & 1, stb);
+          // 4: values, then the split stores into its slot
+          layer1_rt((b - 8) >> 2, (b >> 1) & 1, sth - L_H1);
         }
         if (b & 1) {
           const int rt = (b >> 1) >> 2, s = (b >> 1) & 3;
@@ -782,42 +713,41 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
           }
         }
       };
-      bf16x8 A_c, A_n;
+      AOp A_c, A_n;
       load_ops(0, A_c);
 #pragma unroll
       for (int b = 0; b < 32; ++b) {
         if (b + 1 < 32) load_ops(b + 1, A_n);
         FENCE();
         if ((b & 1) == 0) {
-          const int ot = (b >> 1) & 7;
-          const bf16x8(&bq)[3] = (b >> 1) < 8 ? bq0 : bq1;
-          accW2[ot] = mfma16(A_c, bq[2], accW2[ot]);
-          accW2[ot] = mfma16(A_c, bq[1], accW2[ot]);
-          accW2[ot] = mfma16(A_c, bq[0], accW2[ot]);
+          const int ks = (b >> 1) >> 3, ot = (b >> 1) & 7;
+          // the three products, small terms first
+          accW2[ot] = mfma16h(A_c.l, Bw[ks][0], accW2[ot]);
+          accW2[ot] = mfma16h(A_c.h, Bw[ks][1], accW2[ot]);
+          accW2[ot] = mfma16h(A_c.h, Bw[ks][0], accW2[ot]);
         } else {
           const int rt = (b >> 1) >> 2, s = (b >> 1) & 3, q = rt & 1;
           if (s == 0) dh[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-          const f16x8 Ah = __builtin_bit_cast(f16x8, A_c);
-          dh[q] = mfma16h(Ah, wd[s][1], dh[q]);
-          dh[q] = mfma16h(Ah, wd[s][0], dh[q]);
+          dh[q] = mfma16h(A_c.h, wd[s][1], dh[q]);
+          dh[q] = mfma16h(A_c.h, wd[s][0], dh[q]);
         }
         FENCE();
         ytask(b);
         FENCE();
         A_c = A_n;
       }
-      S8H_STAMP_Y(a, j, w, l, 4);
+      S8G_STAMP_Y(a, j, w, l, 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s) dw1(s, 3);
       if (item_cur)
         sa += sg;
       else
         sb += sg;
-      S8H_STAMP_Y(a, j, w, l, 5);
+      S8G_STAMP_Y(a, j, w, l, 5);
     }
     __syncthreads();
-    S8H_STAMP_Y(a, j, w, l, 6);
-    S8H_STAMP_Y(a, j, w, l, 7);
+    S8G_STAMP_Y(a, j, w, l, 6);
+    S8G_STAMP_Y(a, j, w, l, 7);
     // rotate the pipeline
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];
@@ -827,12 +757,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   // every entry has exactly one producing lane
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
   const float *w3g = P + PL.ow3();
+  // dW2's units 2^(14 - erun) S_H removed (powers of two: exact)
+  const float u2 = __int_as_float((127 + erun - 14) << 23) * (1.0f / SH);
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int o = 16 * ot + 4 * G + j;
-      slab[PL.oW2() + o * kH + 16 * w + li] = accW2[ot][j] * w3g[o];
+      slab[PL.oW2() + o * kH + 16 * w + li] = (accW2[ot][j] * u2) * w3g[o];
     }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -879,19 +811,19 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
 }
 #undef FENCE
 
-}  // namespace s8h
+}  // namespace s8g
 
-hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
+hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)s8h::policy_train_split8wh_kernel,
+    (void)hipFuncSetAttribute((const void *)s8g::policy_train_split8wg_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)s8h::kLds);
+                              (int)s8g::kLds);
     attr = true;
   }
-  hipLaunchKernelGGL(s8h::policy_train_split8wh_kernel, dim3(grid),
-                     dim3(s8h::kThreads), s8h::kLds, s, a);
+  hipLaunchKernelGGL(s8g::policy_train_split8wg_kernel, dim3(grid),
+                     dim3(s8g::kThreads), s8g::kLds, s, a);
   return hipGetLastError();
 }
 

@@ -534,7 +534,9 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 // XH_TRAIN_KERNEL=f32 keeps the f32-MFMA train kernel where the split one
 // would run (A/B measurements and the f32-vs-split tests); for the 64-bin
 // shape the default is the pipelined 8-wave kernel on f16 pairs
-// (policy_split8wh_kernels.hip); =split8wp keeps its all-bf16 form
+// (policy_split8wh_kernels.hip); =split8wg its form with dW2 on f16 pairs
+// from two LDS images (policy_split8wg_kernels.hip); =split8wp keeps its
+// all-bf16 form
 // (policy_split8wp_kernels.hip), =split4p the pipelined 4-wave one
 // (policy_split4p_kernels.hip), =split8w the unpipelined 8-wave one
 // (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel; for
@@ -588,6 +590,13 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
   if (train_kernel_is("split8wp")) {
     if (info) info->name = "policy_train_split8wp_kernel";
     return launch_policy_train_split8wp(a, grid, s);
+  }
+  if (train_kernel_is("split8wg")) {
+    if (info) {
+      info->name = "policy_train_split8wg_kernel";
+      info->math = kMathSplitTrainF16;
+    }
+    return launch_policy_train_split8wg(a, grid, s);
   }
   if (train_kernel_is("split4p")) {
     if (info) info->name = "policy_train_split4p_kernel";

@@ -320,6 +320,8 @@ hipError_t launch_policy_train_split4p(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
+hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
