@@ -531,13 +531,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       float itnA = 0.0f, itnB = 0.0f;
       f32x4 dx0, dgg;
       f32x4 dh[2];
-      auto load_ops = [&](int b, bf16x8 &A) {
-        if (b < 4 || b >= 12) {
-          const int ks = b >= 12, ot = b & 3;
+      // blocks alternate: even bb_ dW2 block d = bb_ / 2 (K-step d / 4,
+      // o-tile d % 4), odd bb_ dH1 block h = bb_ / 2 (r-tile h / 2, K-slice
+      // h % 2)
+      auto load_ops = [&](int bb_, bf16x8 &A) {
+        const int d = bb_ >> 1;
+        if ((bb_ & 1) == 0) {
+          const int ks = d >> 2, ot = d & 3;
           A = ldtr((trm0 ^ (32 * ot)) + L_MASK + 8192 * ks,
                    (trm1 ^ (32 * ot)) + L_MASK + 8192 * ks);
         } else {
-          const int rt = (b - 4) >> 1, s = (b - 4) & 1;
+          const int rt = d >> 1, s = d & 1;
           A = ld8((rdb ^ (64 * s)) + L_MASKH + 4096 * rt);  // f16 bits
         }
       };
@@ -601,9 +605,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
             store_h1(t1, stb, rt);
           }
         }
-        if (b >= 4 && b < 12) {
+        if (b & 1) {
           // dW1 of the previous r-tile (two values per slot), the next rows
-          const int rt = (b - 4) >> 1, s = (b - 4) & 1;
+          const int rt = (b >> 1) >> 1, s = (b >> 1) & 1;
           if (rt > 0) {
             dw1(2 * s, rt - 1);
             dw1(2 * s + 1, rt - 1);
@@ -613,9 +617,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
             dx0 = lds4v(xim + r0);
             dgg = lds4v(gw + r0);
           }
-        } else if (b == 12 || b == 13) {
-          dw1(2 * (b - 12), 3);
-          dw1(2 * (b - 12) + 1, 3);
         }
       };
       bf16x8 A_c, A_n;
@@ -624,14 +625,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       for (int b = 0; b < 16; ++b) {
         if (b + 1 < 16) load_ops(b + 1, A_n);
         FENCE();
-        if (b < 4 || b >= 12) {
-          const int ot = b & 3;
-          const bf16x8(&bq)[3] = b < 4 ? bq0 : bq1;
+        if ((b & 1) == 0) {
+          const int ot = (b >> 1) & 3;
+          const bf16x8(&bq)[3] = (b >> 1) < 4 ? bq0 : bq1;
           accW2[ot] = mfma16(A_c, bq[2], accW2[ot]);
           accW2[ot] = mfma16(A_c, bq[1], accW2[ot]);
           accW2[ot] = mfma16(A_c, bq[0], accW2[ot]);
         } else {
-          const int rt = (b - 4) >> 1, s = (b - 4) & 1, q = rt & 1;
+          const int rt = (b >> 1) >> 1, s = (b >> 1) & 1, q = rt & 1;
           if (s == 0) dh[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
           const f16x8 Ah = __builtin_bit_cast(f16x8, A_c);
           dh[q] = mfma16h(Ah, wd[s][1], dh[q]);
@@ -642,6 +643,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
         FENCE();
         A_c = A_n;
       }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) dw1(jj, 3);  // the last r-tile's
       if (iaA)
         sa += sgA;
       else
