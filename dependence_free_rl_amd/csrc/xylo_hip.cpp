@@ -566,13 +566,13 @@ int apply_env_overrides(xh_trainer *t) {
   hipStream_t s = t->ctx->stream;
   const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
   // runs of consecutive env ids (the map is ordered): one bins copy and one
-  // items copy per run, a single stream synchronisation at the end
-  std::vector<int8_t> rb, ri;
+  // items copy per run from host staging that lives until the single stream
+  // synchronisation at the end (pageable sources)
+  std::vector<std::vector<int8_t>> stage;
   auto it = t->env_override.begin();
   while (it != t->env_override.end()) {
     const size_t first = (size_t)it->first;
-    rb.clear();
-    ri.clear();
+    std::vector<int8_t> rb, ri;
     size_t next = first;
     for (; it != t->env_override.end() && (size_t)it->first == next; ++it, ++next) {
       rb.insert(rb.end(), it->second.begin(), it->second.begin() + BD);
@@ -580,13 +580,20 @@ int apply_env_overrides(xh_trainer *t) {
       for (size_t d = 0; d < D; ++d) item[d] = it->second[BD + d];
       ri.insert(ri.end(), item, item + 4);
     }
-    HIPCHK(hipMemcpyAsync(t->bins + first * BD, rb.data(), rb.size(),
-                          hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(t->items + first * 4, ri.data(), ri.size(),
-                          hipMemcpyHostToDevice, s));
-    // pageable sources: the copies must complete before rb / ri are reused
-    HIPCHK(hipStreamSynchronize(s));
+    stage.push_back(std::move(rb));
+    stage.push_back(std::move(ri));
+    const std::vector<int8_t> &sb = stage[stage.size() - 2], &si = stage.back();
+    hipError_t e = hipMemcpyAsync(t->bins + first * BD, sb.data(), sb.size(),
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(t->items + first * 4, si.data(), si.size(),
+                         hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(s);  // nothing in flight reads `stage` after this
+      return fail(XH_ERR_HIP, "env override upload: %s", hipGetErrorString(e));
+    }
   }
+  HIPCHK(hipStreamSynchronize(s));
   t->env_override.clear();
   return XH_OK;
 }
