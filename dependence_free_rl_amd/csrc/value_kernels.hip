@@ -121,24 +121,34 @@ __device__ __forceinline__ int slab_src(int i, const SlabAlias &al) {
   }
   return i;
 }
+// kSlabRows partial sums per parameter (wave r sums slabs r, r + kSlabRows,
+// ...: the loads of one step are kSlabRows rows apart, and every wave's
+// serial chain is nslab / kSlabRows long), then a fixed-order pairwise tree:
+// deterministic, the same bits run to run
+constexpr int kSlabRows = 16;
 __device__ __forceinline__ float slab_sum(const float *slab, int nslab,
                                           int stride, int n, int i,
                                           int src) {
-  __shared__ float part[4][64];
+  __shared__ float part[kSlabRows][64];
   const int p = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int per = (nslab + 3) / 4, k0 = r * per,
-            k1 = k0 + per < nslab ? k0 + per : nslab;
   float s = 0.0f;
   if (i < n) {
 #pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += slab[(size_t)k * stride + src];
+    for (int k = r; k < nslab; k += kSlabRows) s += slab[(size_t)k * stride + src];
   }
   part[r][p] = s;
   __syncthreads();
-  return (part[0][p] + part[1][p]) + (part[2][p] + part[3][p]);
+  float t[kSlabRows];
+#pragma unroll
+  for (int q = 0; q < kSlabRows; ++q) t[q] = part[q][p];
+#pragma unroll
+  for (int w = kSlabRows / 2; w >= 1; w >>= 1)
+#pragma unroll
+    for (int q = 0; q < w; ++q) t[q] = t[q] + t[q + w];
+  return t[0];
 }
 
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float *slab,
+__global__ __launch_bounds__(64 * kSlabRows) void slab_reduce_kernel(const float *slab,
                                                           int nslab, int stride,
                                                           int n, float *out,
                                                           SlabAlias al) {
@@ -193,7 +203,7 @@ __global__ void opt_kernel(float *p, const float *g, float *m, float *v, int n,
 
 // Single rank: the slab reduce and the optimizer step in one launch (the
 // reduced gradient is still written out for introspection).
-__global__ __launch_bounds__(256) void slab_reduce_opt_kernel(
+__global__ __launch_bounds__(64 * kSlabRows) void slab_reduce_opt_kernel(
     const float *slab, int nslab, int stride, int n, float *out, float *p,
     float *m, float *v, OptStep o, SlabAlias al) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -246,7 +256,7 @@ hipError_t launch_adv_normalize(float *adv, long n, const double *stats,
 
 hipError_t launch_slab_reduce(const float *slab, int nslab, int stride, int n,
                               float *out, hipStream_t s, SlabAlias al) {
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, s,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((n + 63) / 64), dim3(64 * kSlabRows), 0, s,
                      slab, nslab, stride, n, out, al);
   return hipGetLastError();
 }
@@ -255,7 +265,7 @@ hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
                                   int n, float *out, float *params, float *m,
                                   float *v, OptStep o, hipStream_t s,
                                   SlabAlias al) {
-  hipLaunchKernelGGL(slab_reduce_opt_kernel, dim3((n + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(slab_reduce_opt_kernel, dim3((n + 63) / 64), dim3(64 * kSlabRows), 0,
                      s, slab, nslab, stride, n, out, params, m, v, o, al);
   return hipGetLastError();
 }
