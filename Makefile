@@ -12,13 +12,15 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall \
 OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
-            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/policy_split_kernels.o \
-            $(SRC)/policy_split128_kernels.o $(SRC)/policy_split8w_kernels.o $(SRC)/policy_split8wp_kernels.o \
-            $(SRC)/policy_split4p_kernels.o $(SRC)/policy_split8wh_kernels.o \
-            $(SRC)/policy_split8x_kernels.o \
+            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o \
+            $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8x_kernels.o \
             $(SRC)/policy_split4h_kernels.o \
-            $(SRC)/policy_split8wg_kernels.o \
-            $(SRC)/xylo_hip.o
+            $(SRC)/train_select.o $(SRC)/xylo_hip.o
+# superseded train kernels (the config-3 / config-5
+# epoch's earlier forms), kept for A/B runs in the variant library only
+VARIANT_KERNELS := policy_split_kernels policy_split128_kernels \
+            policy_split8w_kernels policy_split8wp_kernels \
+            policy_split4p_kernels policy_split8wg_kernels
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
@@ -35,7 +37,7 @@ REF_APPS := ppo_training ac_training ppo2_training pg_training deep_agent \
 EXAMPLES := $(patsubst examples/%.cc,$(COMPAT)/%,$(wildcard examples/*.cc))
 COMPAT_HDRS := $(shell find include/xylo_compat -name '*.h') include/xylo_hip.h
 
-.PHONY: all lib oracle compat clean diag variant
+.PHONY: all lib oracle compat clean diag variant variants
 all: lib oracle compat
 
 lib: $(LIB)
@@ -59,6 +61,25 @@ $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 
 $(SRC)/xylo_hip.o: $(SRC)/xylo_hip.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(SRC)/train_select.o: $(SRC)/train_select.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the variant library: the product objects + the superseded train kernels,
+# with the dispatch that reaches them (XH_TRAIN_KERNEL=split4w / split8w /
+# split8wp / split4p / split8wg / split128); loaded through XH_LIB_PATH only
+VDIR := build/variants
+VOBJS := $(patsubst %,$(VDIR)/%.o,$(VARIANT_KERNELS))
+$(VDIR)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(VDIR)
+	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@
+$(VDIR)/train_select.o: $(SRC)/train_select.cpp $(HDRS)
+	@mkdir -p $(VDIR)
+	$(HIPCC) $(HIPFLAGS) -DXH_VARIANT_KERNELS=1 -c $< -o $@
+variants: $(OBJS) $(VOBJS) $(VDIR)/train_select.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(VDIR)/libxylo_hip.so \
+	    $(filter-out $(SRC)/train_select.o,$(OBJS)) $(VOBJS) $(VDIR)/train_select.o \
+	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl \

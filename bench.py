@@ -297,6 +297,11 @@ def main():
     avg_ms = ms_pt / max(n_pt, 1)
     # what ran, and the peak of its arithmetic: from the library
     kinfo = tr.kernel_info()
+    if kinfo.get("train_grid_cap"):  # test-only depth control (xh_config)
+        print("bench.py: the trainer ran with train_grid_cap %d; the bench "
+              "measures the library's own grid only" % kinfo["train_grid_cap"],
+              file=sys.stderr)
+        sys.exit(2)
     kt, kr = kinfo["policy_train"], kinfo["rollout_step"]
     split = kt["math"] != "f32_mfma"
     # the split kernels have one shape each: their summaries are keyed by

@@ -40,7 +40,7 @@ class Config(C.Structure):
         ("lambda_", C.c_float), ("clip_eps", C.c_float),
         ("rng_state", C.c_uint32), ("kl_beta", C.c_float),
         ("kl_target", C.c_float), ("adv_normalize", C.c_int),
-        ("lr_scale_rows", C.c_int)]
+        ("lr_scale_rows", C.c_int), ("train_grid_cap", C.c_int)]
 
 
 class Eval(C.Structure):

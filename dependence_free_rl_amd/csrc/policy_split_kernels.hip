@@ -2,9 +2,10 @@
 // 64-bin 2-D [128,128] policy (BASELINE configs 3 and 4) with its three
 // 128x128 GEMMs on the bf16 matrix cores at f32 accuracy (xh_split.h: each
 // f32 operand split exactly into three bf16 parts; six bf16 MFMAs per K = 16
-// slice in place of eight f32 ones).  The 128-bin 3-D one (config 5) is
-// policy_split128_kernels.hip; this file is compiled with the VGPR form of
-// the MFMAs (Makefile).
+// slice in place of eight f32 ones).  Round 2's config-3 kernel, superseded
+// by policy_split8wh_kernels.hip: built only into the variant library
+// (`make variants`, XH_TRAIN_KERNEL=split4w) for A/B runs; compiled with the
+// VGPR form of the MFMAs (Makefile).
 //
 // Same math as policy_train8_kernel (policy_kernels.hip): per 64-row group
 // (one env, its 64 bins) layer 1 (conv1d_1 F0 -> 128, item folded into the
@@ -531,85 +532,10 @@ __global__ __launch_bounds__(kThreads, 1) void policy_train_split_kernel(PolicyT
 
 }  // namespace split
 
-// XH_TRAIN_KERNEL=f32 keeps the f32-MFMA train kernel where the split one
-// would run (A/B measurements and the f32-vs-split tests); for the 64-bin
-// shape the default is the pipelined 8-wave kernel on f16 pairs
-// (policy_split8wh_kernels.hip); =split8wg its form with dW2 on f16 pairs
-// from two LDS images (policy_split8wg_kernels.hip); =split8wp keeps its
-// all-bf16 form
-// (policy_split8wp_kernels.hip), =split4p the pipelined 4-wave one
-// (policy_split4p_kernels.hip), =split8w the unpipelined 8-wave one
-// (policy_split8w_kernels.hip) and =split4w this file's 4-wave kernel; for
-// the 128-bin 3-D shape the default is the pipelined 8-wave kernel
-// (policy_split8x_kernels.hip) and =split128 keeps the 4-wave one
-// (policy_split128_kernels.hip); the 32-bin 1-D [64,64] shape runs the
-// pipelined 4-wave kernel on f16 pairs (policy_split4h_kernels.hip).
-// Diagnostic overrides, read per launch and reported by
-// xh_trainer_kernel_info.
-bool train_split_enabled() {
-  const char *e = std::getenv("XH_TRAIN_KERNEL");
-  return !(e && e[0] == 'f');
-}
-static bool train_kernel_is(const char *name) {
-  const char *e = std::getenv("XH_TRAIN_KERNEL");
-  return e && std::strcmp(e, name) == 0;
-}
-
-bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
-  const bool algo = a.algo == kPPO || a.algo == kAC;
-  if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
-    return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
-  return algo && H1 == 128 && H2 == 128 &&
-         ((a.env.B == split::kB && a.env.D == split::kD) ||
-          (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims));
-}
-
-hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
-                                     hipStream_t s, KernelInfo *info) {
-  if (info) info->math = kMathSplitTrain;
-  if (a.env.B == kSplit4hBins) {
-    if (info) {
-      info->name = "policy_train_split4h_kernel";
-      info->math = kMathSplitTrainF16;
-    }
-    return launch_policy_train_split4h(a, grid, s);
-  }
-  if (a.env.B == kSplit128Bins) {
-    if (info) info->math = kMathSplitTrainF16;
-    if (!train_kernel_is("split128")) {
-      if (info) info->name = "policy_train_split8x_kernel";
-      return launch_policy_train_split8x(a, grid, s);
-    }
-    if (info) info->name = "policy_train_split128_kernel";
-    return launch_policy_train_split128(a, grid, s);
-  }
-  if (train_kernel_is("split8w")) {
-    if (info) info->name = "policy_train_split8w_kernel";
-    return launch_policy_train_split8w(a, grid, s);
-  }
-  if (train_kernel_is("split8wp")) {
-    if (info) info->name = "policy_train_split8wp_kernel";
-    return launch_policy_train_split8wp(a, grid, s);
-  }
-  if (train_kernel_is("split8wg")) {
-    if (info) {
-      info->name = "policy_train_split8wg_kernel";
-      info->math = kMathSplitTrainF16;
-    }
-    return launch_policy_train_split8wg(a, grid, s);
-  }
-  if (train_kernel_is("split4p")) {
-    if (info) info->name = "policy_train_split4p_kernel";
-    return launch_policy_train_split4p(a, grid, s);
-  }
-  if (!train_kernel_is("split4w")) {
-    if (info) {
-      info->name = "policy_train_split8wh_kernel";
-      info->math = kMathSplitTrainF16;
-    }
-    return launch_policy_train_split8wh(a, grid, s);
-  }
-  if (info) info->name = "policy_train_split_kernel";
+// The variant library's entry point for this kernel (train_select.cpp,
+// XH_TRAIN_KERNEL=split4w; `make variants`).
+hipError_t launch_policy_train_split4w(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)split::policy_train_split_kernel,
@@ -618,8 +544,7 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
     attr = true;
   }
   hipLaunchKernelGGL(split::policy_train_split_kernel, dim3(grid),
-                     dim3(split::kThreads),
-                     split::kLds, s, a);
+                     dim3(split::kThreads), split::kLds, s, a);
   return hipGetLastError();
 }
 

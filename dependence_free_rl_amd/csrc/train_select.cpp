@@ -1,0 +1,113 @@
+// train_select.cpp -- which policy train kernel an epoch launches (host code).
+//
+// Product kernels (libxylo_hip.so), f16 pairs + the exact bf16 split
+// (DESIGN.md §3.0a-d):
+//   64 bins, 2-D, [128,128] (configs 3 / 4)  policy_train_split8wh_kernel
+//   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
+//   32 bins, 1-D, [64,64] (config 2)         policy_train_split4h_kernel
+// and the f32-MFMA kernels of policy_kernels.hip for every other shape, for
+// KL-PPO, and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
+// kernels' tests).
+//
+// The superseded config-3 / config-5 forms (split4w, split8w, split8wp,
+// split4p, split8wg, split128) are built only into the variant library
+// (`make variants` -> build/variants/libxylo_hip.so, loaded through
+// XH_LIB_PATH for A/B runs, never by the product path): this file is compiled
+// there with XH_VARIANT_KERNELS=1.  In the product library an override that
+// names one of them fails the epoch with hipErrorNotSupported.
+#include <cstdlib>
+#include <cstring>
+
+#include "xh_kernels.h"
+
+#ifndef XH_VARIANT_KERNELS
+#define XH_VARIANT_KERNELS 0
+#endif
+
+namespace xh {
+
+#if XH_VARIANT_KERNELS
+hipError_t launch_policy_train_split4w(const PolicyTrainArgs &a, int grid,
+                                       hipStream_t s);
+#endif
+
+// Diagnostic override, read per launch and reported by xh_trainer_kernel_info.
+bool train_split_enabled() {
+  const char *e = std::getenv("XH_TRAIN_KERNEL");
+  return !(e && e[0] == 'f');
+}
+static const char *train_override() {
+  const char *e = std::getenv("XH_TRAIN_KERNEL");
+  return e && *e ? e : nullptr;
+}
+#if XH_VARIANT_KERNELS
+static bool train_kernel_is(const char *name) {
+  const char *e = train_override();
+  return e && std::strcmp(e, name) == 0;
+}
+#endif
+
+bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
+  const bool algo = a.algo == kPPO || a.algo == kAC;
+  if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
+    return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
+  return algo && H1 == 128 && H2 == 128 &&
+         ((a.env.B == 64 && a.env.D == 2) ||
+          (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims));
+}
+
+hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
+                                     hipStream_t s, KernelInfo *info) {
+  KernelInfo dummy;
+  if (!info) info = &dummy;
+  info->math = kMathSplitTrainF16;
+  const char *ov = train_override();
+  if (a.env.B == kSplit4hBins) {
+    info->name = "policy_train_split4h_kernel";
+    return launch_policy_train_split4h(a, grid, s);
+  }
+  if (a.env.B == kSplit128Bins) {
+    if (!ov) {
+      info->name = "policy_train_split8x_kernel";
+      return launch_policy_train_split8x(a, grid, s);
+    }
+#if XH_VARIANT_KERNELS
+    if (train_kernel_is("split128")) {
+      info->name = "policy_train_split128_kernel";
+      return launch_policy_train_split128(a, grid, s);
+    }
+#endif
+  } else {
+    if (!ov) {
+      info->name = "policy_train_split8wh_kernel";
+      return launch_policy_train_split8wh(a, grid, s);
+    }
+#if XH_VARIANT_KERNELS
+    if (train_kernel_is("split8wg")) {
+      info->name = "policy_train_split8wg_kernel";
+      return launch_policy_train_split8wg(a, grid, s);
+    }
+    info->math = kMathSplitTrain;  // the all-bf16 forms
+    if (train_kernel_is("split8w")) {
+      info->name = "policy_train_split8w_kernel";
+      return launch_policy_train_split8w(a, grid, s);
+    }
+    if (train_kernel_is("split8wp")) {
+      info->name = "policy_train_split8wp_kernel";
+      return launch_policy_train_split8wp(a, grid, s);
+    }
+    if (train_kernel_is("split4p")) {
+      info->name = "policy_train_split4p_kernel";
+      return launch_policy_train_split4p(a, grid, s);
+    }
+    if (train_kernel_is("split4w")) {
+      info->name = "policy_train_split_kernel";
+      return launch_policy_train_split4w(a, grid, s);
+    }
+#endif
+  }
+  info->name = nullptr;
+  return hipErrorNotSupported;  // an override this library was built without
+}
+
+}  // namespace xh

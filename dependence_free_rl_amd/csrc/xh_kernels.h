@@ -303,7 +303,9 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
                                KernelInfo *info = nullptr);
 // The f32-accurate split train kernels for the 64-bin 2-D and 128-bin 3-D
 // [128,128] shapes and the 32-bin 1-D [64,64] one (dispatch in
-// policy_split_kernels.hip); XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.
+// train_select.cpp); XH_TRAIN_KERNEL=f32 selects the f32-MFMA ones.  The
+// launchers of the superseded forms (split128 / 8w / 8wp / 4p / 8wg) are
+// linked only into the variant library (`make variants`).
 constexpr int kSplit128Bins = 128, kSplit128Dims = 3;
 constexpr int kSplit4hBins = 32;
 bool train_split_enabled();

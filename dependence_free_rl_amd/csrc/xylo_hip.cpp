@@ -1431,6 +1431,8 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
                   c.env_offset, c.num_envs, c.num_envs_global);
     if (c.bins * 2 * c.dims > 768)
       return fail(XH_ERR_INVALID, "value input %d > 768", c.bins * 2 * c.dims);
+    if (c.train_grid_cap < 0)
+      return fail(XH_ERR_INVALID, "train_grid_cap %d < 0", c.train_grid_cap);
     HIPCHK(hipSetDevice(ctx->device));
 
     auto *t = new xh_trainer;
@@ -1480,6 +1482,8 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2,
                                        c.algo == XH_KLPPO);
     const int groups = (int)(T * N / (size_t)G);
+    if (c.train_grid_cap > 0 && t->pslab_n > c.train_grid_cap)
+      t->pslab_n = c.train_grid_cap;  // test-only depth control (xylo_hip.h)
     if (t->pslab_n > groups) t->pslab_n = groups;
     t->pslab_stride = (t->np + 63) & ~63;
     t->vslab_n = 256;
@@ -1860,6 +1864,9 @@ int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap) {
     if (!t || !buf || cap == 0) return fail(XH_ERR_INVALID, "null arg");
     const std::string js = "{\"rollout_step\": " + kernel_json(t->last_rollout) +
                            ", \"policy_train\": " + kernel_json(t->last_train) +
+                           ", \"train_grid\": " + std::to_string(t->pslab_n) +
+                           ", \"train_grid_cap\": " +
+                           std::to_string(t->cfg.train_grid_cap) +
                            ", \"overrides\": {" + env_json("XH_TRAIN_KERNEL") +
                            ", " + env_json("XH_ROLLOUT_KERNEL") + "}}";
     if (js.size() + 1 > cap)

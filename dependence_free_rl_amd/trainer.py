@@ -200,7 +200,7 @@ class Trainer:
                  lr_policy=None, lr_value=None, wd_policy=None, wd_value=None,
                  gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
                  num_envs_global=None, env_offset=0, adv_normalize=False,
-                 lr_scale_rows=False):
+                 lr_scale_rows=False, train_grid_cap=0):
         cfg = _lib.Config()
         a = ALGOS[algo]
         _lib.lib.xh_config_default(C.byref(cfg), a, bins, dims, num_envs, steps)
@@ -223,6 +223,8 @@ class Trainer:
         # opt-in, off in the reference configuration (xh_config)
         cfg.adv_normalize = int(bool(adv_normalize))
         cfg.lr_scale_rows = int(bool(lr_scale_rows))
+        # test-only: cap on the train workgroups (accumulation depth tests)
+        cfg.train_grid_cap = int(train_grid_cap)
         self.cfg = cfg
         self.ctx = ctx
         self.B, self.D, self.N, self.T = bins, dims, num_envs, steps

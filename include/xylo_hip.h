@@ -115,6 +115,14 @@ typedef struct {
   int lr_scale_rows;   /* 1: both optimizers apply lr / rows, rows = T *
                           num_envs_global, i.e. SGD on the mean instead of the
                           reference's sum over rows (nn.h:94-98, 624) */
+  /* Test-only: 0 (default) = the policy train kernels' own grid (one or two
+     workgroups per CU); > 0 caps the number of train workgroups, so that a
+     batch the oracle can check in seconds runs each workgroup over as many
+     row groups as the benchmark's full batch does (the f32 accumulation
+     depth of the per-workgroup gradient slabs).  Reported by
+     xh_trainer_kernel_info ("train_grid", "train_grid_cap"); bench.py
+     refuses a trainer with a cap. */
+  int train_grid_cap;
 } xh_config;
 
 /* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */

@@ -1,0 +1,141 @@
+"""Gradient accumulation at the benchmark's depth, against the oracle.
+
+The train kernels give every workgroup a run of row groups (64-row groups at
+configs 3 / 2, 64-row units at config 5) and accumulate its dW2 / dW1 sums in
+f32 registers across all of them before writing one gradient slab
+(policy_split8wh / 8x / 4h_kernels.hip).  The benchmark's full batches run
+each workgroup over J = 512 groups (config 3: 131072 / 256), >= 512 units
+(config 5) and 16 groups (config 2); the oracle-sized batches of the other
+parity tests stop at J <= 6.  `train_grid_cap` (xh_config, test-only; the
+bench refuses it) shrinks the train grid so that a batch the oracle checks in
+seconds runs at the same J.  Reference: the per-bin row sums of
+convolution1d_1_layer::gradient (/root/reference/xylo/nn.h:163-186) in
+ppo_learner / actor_critic_learner (policy_gradient.h:150-185, 289-307).
+
+Every epoch-0 gradient is held to the tight budget of conftest (median <= 1,
+p99 <= 100 units of u * sum|terms| against the oracle's double sums), at every
+J; epochs 1..k-1 (parameters each side updated itself) to the drift budget.
+Each comparison is logged with its J (grad_units.jsonl, `depth ...`).
+"""
+import numpy as np
+import pytest
+
+from conftest import (GRAD_UNITS_P99_DRIFT, assert_close, assert_grad_close,
+                      assert_grad_units)
+
+pytestmark = pytest.mark.gpu
+
+# label, algo, B, D, widths, N, T, train_grid_cap values (0 = the default
+# grid), rows per unit of the kernel's loop (one J step)
+DEPTH_CASES = [
+    # config-3 shape: 512 64-row groups; J = 2 (default grid 256), 32, 128, 512
+    ("c3", "ppo", 64, 2, (128, 128), 128, 4, (0, 16, 4, 1)),
+    # config-5 shape: 768 envs = 1536 64-row units; J = 6, 64, 512, 1536 units
+    ("c5", "ac", 128, 3, (128, 128), 96, 8, (0, 24, 3, 1)),
+    # config-2 shape: 1536 two-env groups; J = 3 (default grid 512), 16, 512, 1536
+    ("c2", "ppo", 32, 1, (64, 64), 768, 4, (0, 96, 3, 1)),
+]
+KERNELS = {64: "policy_train_split8wh_kernel", 128: "policy_train_split8x_kernel",
+           32: "policy_train_split4h_kernel"}
+
+
+def _oracle(algo, B, D, N, T, widths, pp, vp, x0):
+    from oracle import pyoracle as po
+    head = po.OR_SOFTMAX_XENT if algo == "ac" else po.OR_SOFTMAX
+    return po.Trainer({"ppo": po.OR_PPO, "ac": po.OR_AC}[algo], B, D, N, T,
+                      po.perbin_model(2 * D, list(widths), head), pp,
+                      po.full_model(B * 2 * D, [64, 32], 1), vp,
+                      lr_pi=1e-5 if algo == "ac" else 1e-4,
+                      lr_v=1e-4 if algo == "ac" else 1e-5, x0=x0)
+
+
+def _units_per_group(B):
+    # the kernels' loop unit: a 64-row group (64 // B envs) or, at 128 bins,
+    # one 64-row half of an env
+    return 2 if B == 128 else 1
+
+
+@pytest.mark.parametrize("label,algo,B,D,widths,N,T,caps", DEPTH_CASES,
+                         ids=[c[0] for c in DEPTH_CASES])
+def test_grad_accumulation_depth(ctx, label, algo, B, D, widths, N, T, caps):
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_POLICY_GRADS,
+                                                BUF_VALUE_GRAD)
+    x0 = 20260417
+    pp = init_policy(D, *widths, seed=41)
+    vp = init_value(B, D, seed=42)
+    orc = _oracle(algo, B, D, N, T, widths, pp, vp, x0)
+    orc.rollout()
+    orc.learn()
+    o_choice = orc.buf(po.BUF_STEP_CHOICE).reshape(N, T).T
+    ref = np.asarray(orc.buf(po.BUF_POLICY_GRADS))
+    mag = np.asarray(orc.buf(po.BUF_POLICY_GRADS_MAG))
+    rows = len(orc.buf(po.BUF_ROW_ENV))
+    groups = N * T * B // 64 if B <= 64 else N * T  # kernel work items
+    seen = []
+    for cap in caps:
+        tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
+                     widths=widths, rng_state=x0, train_grid_cap=cap)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        tr.rollout()
+        np.testing.assert_array_equal(tr.buffer(BUF_ACTION), o_choice)
+        tr.learn()
+        k = tr.kernel_info()
+        assert k["policy_train"]["kernel"] == KERNELS[B], k
+        assert k["train_grid_cap"] == cap, k
+        grid = k["train_grid"]
+        assert cap == 0 or grid == min(cap, groups), (cap, grid, groups)
+        J = -(-groups // grid) * _units_per_group(B)  # loop steps of workgroup 0
+        seen.append(J)
+        assert_close(tr.buffer(BUF_VALUE_GRAD), orc.buf(po.BUF_VALUE_GRAD),
+                     what="value_grad")
+        npi = tr.num_params(POLICY)
+        dev = tr.buffer(BUF_POLICY_GRADS).reshape(-1, npi)
+        r, m = ref.reshape(-1, npi), mag.reshape(-1, npi)
+        assert_grad_close(dev.ravel(), ref, mag, n_terms=rows * B,
+                          what="depth %s J=%d" % (label, J))
+        for ep in range(dev.shape[0]):
+            budget = {} if ep == 0 else {"p99_units": GRAD_UNITS_P99_DRIFT}
+            assert_grad_units(dev[ep], r[ep], m[ep],
+                              what="depth %s %s B%d D%d N%d T%d grid=%d J=%d "
+                                   "epoch%d" % (label, algo, B, D, N, T, grid,
+                                                J, ep), **budget)
+        tr.close()
+    # the deepest case reaches the benchmark's depth
+    bench_depth = {"c3": 512, "c5": 512, "c2": 16}[label]
+    assert max(seen) >= bench_depth, (seen, bench_depth)
+
+
+@pytest.mark.parametrize("algo,B,D,N,T", [("ppo", 64, 2, 32, 4),
+                                         ("ac", 128, 3, 8, 8)])
+def test_free_running_drift(ctx, algo, B, D, N, T):
+    """Three iterations with no re-synchronisation of the oracle to the
+    device's parameters at the config-3 / config-5 shapes: the sampled
+    trajectories stay identical and both nets' parameters stay within the
+    1e-4 parity tolerance of the oracle's after every iteration (the drift of
+    three learn() calls of the f16-pair / bf16-split kernels)."""
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import BUF_ACTION
+    widths, x0 = (128, 128), 13579
+    pp, vp = init_policy(D, *widths, seed=51), init_value(B, D, seed=52)
+    tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
+                 widths=widths, rng_state=x0)
+    tr.set_params(POLICY, pp)
+    tr.set_params(VALUE, vp)
+    orc = _oracle(algo, B, D, N, T, widths, pp, vp, x0)
+    for it in range(3):
+        tr.rollout()
+        orc.rollout()
+        np.testing.assert_array_equal(tr.buffer(BUF_ACTION),
+                                      orc.buf(po.BUF_STEP_CHOICE).reshape(N, T).T)
+        tr.learn()
+        orc.learn()
+        ep = assert_close(tr.params(POLICY), orc.params(0),
+                          what="free-running it%d policy params" % it)
+        ev = assert_close(tr.params(VALUE), orc.params(1),
+                          what="free-running it%d value params" % it)
+        print("free-running %s B%d it%d: policy %.3g value %.3g (scaled max err)"
+              % (algo, B, it, ep, ev))

@@ -18,6 +18,22 @@ from conftest import (HEADLINE_TRAIN_KERNEL, assert_close, assert_grad_close,
 
 pytestmark = pytest.mark.gpu
 
+# (relative L2, worst entry / max |g|) between the shard sum and the full
+# batch at B = 64, n = 16384 (no oracle at that size): about 3x the measured
+# values (r03: 2.9e-4 relative L2; profiles/r04*_shard_sums.jsonl)
+SHARD_SUM_LIMITS_B64 = (1e-3, 4e-3)
+
+
+def _log_shard_sum(B, n, it, rel, worst):
+    import json
+    import os
+    from conftest import REPO
+    print("shards B%d n%d it%d: rel L2 %.3g, worst %.3g" % (B, n, it, rel, worst))
+    d = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, "shard_sums.jsonl"), "a") as f:
+            f.write(json.dumps({"B": B, "n": n, "it": it, "rel_l2": rel,
+                                "worst_rel": worst}) + "\n")
 
 
 @pytest.mark.parametrize("B,D,widths,n", [
@@ -99,13 +115,13 @@ def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
             # at this size: a sanity bound (the oracle-pinned check of the
             # same kernels is the n = 128 case).  Policy-gradient entries
             # cancel to ~1e-3 of their sum |terms| (conftest), so at 8.4 M
-            # rows two summation orders differ by ~1e-4 of |g| (measured
-            # 2.9e-4 relative L2 at 64 bins, 2e-6 at 8 bins)
+            # rows two summation orders differ by ~1e-4 of |g|.  Limits =
+            # about 3x the measured values (r03: 2.9e-4 relative L2 at 64
+            # bins, 2e-6 at 8 bins; the measured pair is logged per run)
             rel = np.linalg.norm(g - f) / np.linalg.norm(f)
             worst = np.abs(g - f).max() / np.abs(f).max()
-            lim = (1e-5, 1e-4) if B == 8 else (2e-3, 4e-3)
-            print("shards B%d n%d it%d: rel L2 %.3g, worst %.3g" % (B, n, it, rel,
-                                                                  worst))
+            lim = (1e-5, 1e-4) if B == 8 else SHARD_SUM_LIMITS_B64
+            _log_shard_sum(B, n, it, rel, worst)
             assert rel <= lim[0] and worst <= lim[1], (rel, worst)
 
 
