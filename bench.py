@@ -117,11 +117,18 @@ def cpu_baseline():
     8(d): the reference path is single-threaded, so a whole host runs it as
     that many independent processes).  About 2 x 8 s."""
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    # config 3 (64 bins, 2-D): the harness built against the reference's own
+    # bin_packing.h with num_bins = 64, i.e. bp::environment / bp::agent
+    # themselves (oracle/Makefile); the other shapes run gen_env<B,D>
+    bp64 = os.path.join(REPO, "oracle", "_ref", "ref_harness_bp64")
+    env_src = "gen_env<%d,%d>" % (B, D)
+    if B == 64 and D == 2 and os.path.exists(bp64):
+        harness, env_src = bp64, "bp::environment (bin_packing.h, num_bins = 64)"
     n_env, iters = 16, max(1, REF_ITERS // 3)
     learner = "ppo_learner" if ALGO == "ppo" else "actor_critic_learner"
-    sample = ("reference %s, %d envs x T=%d x %d iterations per process, "
-              "B=%d D=%d [%d,%d], single-threaded processes" % (
-                  learner, n_env, T, iters, B, D, H1, H2))
+    sample = ("reference %s on %s, %d envs x T=%d x %d iterations per "
+              "process, B=%d D=%d [%d,%d], single-threaded processes" % (
+                  learner, env_src, n_env, T, iters, B, D, H1, H2))
     if os.path.exists(harness):
         try:
             out = subprocess.run(_harness_cmd(harness, n_env, iters, 1),

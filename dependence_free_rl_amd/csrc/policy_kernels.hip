@@ -2354,7 +2354,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
     }                                                                        \
     const int ng = a.b.N / S::G;                                             \
     if constexpr (S::B == 128 && S::NIT == 4 && S::NOT == 4) {               \
-      if (rollout_split()) {                                                 \
+      if (rollout_split() && !a.wide) {                                      \
         static bool sattr = false;                                           \
         if (!sattr) {                                                        \
           (void)hipFuncSetAttribute((const void *)rollout_split128_kernel<S>,\
@@ -2393,7 +2393,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
       }                                                                      \
     }                                                                        \
     if constexpr (S::B == 64 && S::NIT == 4 && S::NOT == 4) {                \
-      if (rollout_split()) {                                                 \
+      if (rollout_split() && !a.wide) {                                      \
         static bool sattr = false;                                           \
         if (!sattr) {                                                        \
           (void)hipFuncSetAttribute((const void *)rollout_split_kernel<S>,   \
@@ -2479,7 +2479,8 @@ hipError_t launch_policy_train(const PolicyTrainArgs &a, int H1, int H2,
   KernelInfo dummy;
   if (!info) info = &dummy;
   info->math = kMathF32Mfma;
-  if (policy_train_split_supported(a, H1, H2) && train_split_enabled())
+  if (policy_train_split_supported(a, H1, H2) && train_split_enabled() &&
+      !a.wide)
     return launch_policy_train_split(a, grid, s, info);
 #define X(XB, XD, XH1, XH2)                                                  \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \

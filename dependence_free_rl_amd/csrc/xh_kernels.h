@@ -68,6 +68,8 @@ struct RolloutArgs {
   float *logits_out;      // optional [N][B] (debug / parity)
   float *probs_out;       // optional [N][B]
   float *qold_out;        // KL-PPO: [T][N][B] the sampled distribution
+  int wide;  // slot t holds a bin below -capacity: the f32-MFMA kernels run
+             // (the f16-pair ones bound |bins / capacity| by 1)
 };
 
 struct PolicyTrainArgs {
@@ -79,6 +81,8 @@ struct PolicyTrainArgs {
   const float *adv;  // [T][N]
   float *slab;       // [gridDim.x][slab_stride]
   int slab_stride;
+  int wide;          // a slot of the batch holds a bin below -capacity: the
+                     // f32-MFMA kernels run (RolloutArgs::wide)
   int ablate;        // diagnostic build only (XH_ABLATE, make diag): bit0 skip
                      // dW2, bit1 skip dH1/dW1, bit2 skip layer-2 fwd, bit3
                      // skip softmax/loss; folded away in the product build

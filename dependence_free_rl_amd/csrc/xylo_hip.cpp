@@ -174,6 +174,12 @@ struct xh_trainer {
   // so learn() refuses a batch that reads a slot with any other item
   // (xh_trainer_set_buffer accepts them for rollout-only use).
   std::vector<char> items_ok;
+  // Slots of `bins` that may hold a bin below -capacity (an overflowed state
+  // the reference reaches by applying to a game-over env again, bin_packing.h:
+  // 53-63, uploaded by hand).  The f16-pair kernels bound every observation
+  // feature by |bins / capacity| <= 1, so a rollout step
+  // or learn() that reads such a slot runs the f32-MFMA kernels instead.
+  std::vector<char> bins_wide;
   // what the last rollout step / policy epoch launched (xh_trainer_kernel_info)
   xh::KernelInfo last_rollout, last_train;
   bool timing = false;
@@ -561,6 +567,29 @@ int do_pg_learn(xh_trainer *t);
 // Pending xh_trainer_set_env_state writes -> slot 0 (the rollout's S_0).  The
 // host vectors stay alive until the stream has consumed them (synchronised
 // before the map is cleared).
+// items_ok[0] / bins_wide[0] from the device's slot 0 (after host writes that
+// replaced part of it)
+int rescan_slot0(xh_trainer *t) {
+  const size_t N = t->N(), BD = t->BD(), D = (size_t)t->cfg.dims;
+  std::vector<int8_t> b(N * BD), it(N * 4);
+  HIPCHK(copy_to_host(b.data(), t->bins, b.size(), t->ctx->stream));
+  HIPCHK(copy_to_host(it.data(), t->items, it.size(), t->ctx->stream));
+  HIPCHK(hipStreamSynchronize(t->ctx->stream));
+  char ok = 1, wide = 0;
+  for (size_t e = 0; e < N; ++e) {
+    bool is_a = true, is_b = true;
+    for (size_t d = 0; d < D; ++d) {
+      is_a &= it[e * 4 + d] == t->env.item_a[d];
+      is_b &= it[e * 4 + d] == t->env.item_b[d];
+    }
+    if (!is_a && !is_b) ok = 0;
+  }
+  for (int8_t v : b) wide |= v < -kBinCapacity;
+  t->items_ok[0] = ok;
+  t->bins_wide[0] = wide;
+  return XH_OK;
+}
+
 int apply_env_overrides(xh_trainer *t) {
   if (t->env_override.empty()) return XH_OK;
   hipStream_t s = t->ctx->stream;
@@ -594,7 +623,15 @@ int apply_env_overrides(xh_trainer *t) {
     }
   }
   HIPCHK(hipStreamSynchronize(s));
+  bool wide = false;
+  for (const auto &kv : t->env_override)
+    for (size_t i = 0; i < BD; ++i) wide |= kv.second[i] < -kBinCapacity;
   t->env_override.clear();
+  // slot 0's flags: the overrides are whole item-table entries, but envs they
+  // did not touch keep what an earlier set_buffer left -> re-read the slot
+  // when either flag was off its default
+  if (!t->items_ok[0] || t->bins_wide[0]) return rescan_slot0(t);
+  if (wide) t->bins_wide[0] = 1;
   return XH_OK;
 }
 
@@ -606,6 +643,7 @@ int do_rollout(xh_trainer *t) {
     t->items_ok.assign(T + 1, 0);
     t->items_ok[0] = 1;
   }
+  if (t->bins_wide.size() != T + 1) t->bins_wide.assign(T + 1, 0);
   if (t->need_shift) {  // replay_buffer::forget(): open trajectories continue
     HIPCHK(hipMemcpyAsync(t->bins, t->bins + T * N * t->BD(), N * t->BD(),
                           hipMemcpyDeviceToDevice, s));
@@ -613,6 +651,7 @@ int do_rollout(xh_trainer *t) {
                           hipMemcpyDeviceToDevice, s));
     t->need_shift = false;
     t->items_ok[0] = t->items_ok[T];
+    t->bins_wide[0] = t->bins_wide[T];
   }
   CHK(apply_env_overrides(t));  // whole item-table entries only
   xh::RolloutArgs a{};
@@ -624,6 +663,7 @@ int do_rollout(xh_trainer *t) {
   a.qold_out = t->qold;  // KL-PPO only (nullptr otherwise)
   for (int step = 0; step < (int)T; ++step) {
     a.t = step;
+    a.wide = t->bins_wide[step];
     const bool last = step == (int)T - 1;
     a.logits_out = last ? t->logits : nullptr;
     a.probs_out = last ? t->probs : nullptr;
@@ -632,6 +672,7 @@ int do_rollout(xh_trainer *t) {
                                      t->rgrid, s, &t->last_rollout);
     }));
     t->items_ok[step + 1] = 1;  // items drawn from the table (get_item)
+    t->bins_wide[step + 1] = 0;  // apply + reset on game over: bins >= 0
   }
   return XH_OK;
 }
@@ -753,6 +794,8 @@ int do_learn(xh_trainer *t) {
   pa.adv = t->adv;
   pa.slab = t->pslab;
   pa.slab_stride = t->pslab_stride;
+  for (size_t sl = 0; sl < t->T() && sl < t->bins_wide.size(); ++sl)
+    pa.wide |= t->bins_wide[sl];
   {
     // XH_ABLATE drops whole phases (wrong results by design): honoured by the
     // diagnostic build only, refused by the product library
@@ -1728,12 +1771,17 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
     }
     const bool states = t->cfg.algo != XH_PG &&
                         (which == XH_BUF_BINS || which == XH_BUF_ITEMS);
+    std::vector<char> wide;
     if (states && which == XH_BUF_BINS) {  // as xh_trainer_set_env_state
       const int8_t *b = static_cast<const int8_t *>(host);
-      for (size_t i = 0; i < bytes; ++i)
-        if (b[i] < -kBinCapacity || b[i] > kBinCapacity)
-          return fail(XH_ERR_INVALID, "bin value %d outside [-%d, %d]", b[i],
-                      kBinCapacity, kBinCapacity);
+      const size_t per_slot = t->N() * t->BD();
+      wide.assign(t->T() + 1, 0);
+      for (size_t i = 0; i < bytes; ++i) {
+        if (b[i] > kBinCapacity)
+          return fail(XH_ERR_INVALID, "bin value %d above the capacity %d",
+                      b[i], kBinCapacity);
+        if (b[i] < -kBinCapacity) wide[i / per_slot] = 1;
+      }
     }
     std::vector<char> ok;
     if (states && which == XH_BUF_ITEMS) {
@@ -1759,6 +1807,7 @@ int xh_trainer_set_buffer(xh_trainer *t, int which, const void *host,
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
     if (which == XH_BUF_BINS || which == XH_BUF_ITEMS) t->need_shift = false;
     if (!ok.empty()) t->items_ok = std::move(ok);
+    if (!wide.empty()) t->bins_wide = std::move(wide);
     return XH_OK;
   });
 }
@@ -1953,12 +2002,14 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
                   t->cfg.num_envs);
     const size_t BD = t->BD(), D = (size_t)t->cfg.dims;
     // negative values are the overflowed (game-over) states an apply by hand
-    // leaves (bin_packing.h:53-63); an item is at most the capacity, so a bin
-    // is never below -capacity
+    // leaves (bin_packing.h:53-63); applying to a game-over env again keeps
+    // subtracting, so any int8 value up to the capacity is a reachable state
+    // (below -capacity the next rollout step / learn() run the f32 kernels,
+    // bins_wide)
     for (size_t i = 0; i < (size_t)count * BD; ++i)
-      if (bins[i] < -kBinCapacity || bins[i] > kBinCapacity)
-        return fail(XH_ERR_INVALID, "bin value %d outside [-%d, %d]", bins[i],
-                    kBinCapacity, kBinCapacity);
+      if (bins[i] > kBinCapacity)
+        return fail(XH_ERR_INVALID, "bin value %d above the capacity %d",
+                    bins[i], kBinCapacity);
     // a whole item-table entry (the train kernels carry the item columns of
     // dW1 as per-entry sums)
     for (int e = 0; e < count; ++e) {
@@ -2187,10 +2238,12 @@ int xh_venv_set(xh_venv *v, int which, const void *host, size_t bytes) {
     }
     if (which == XH_VENV_BINS) {
       const int8_t *b = static_cast<const int8_t *>(host);
+      // any int8 value up to the capacity: the venv computes in int / f32
+      // (an apply to a game-over env keeps subtracting, bin_packing.h:53-63)
       for (size_t i = 0; i < bytes; ++i)
-        if (b[i] < -kBinCapacity || b[i] > kBinCapacity)
-          return fail(XH_ERR_INVALID, "venv: bin value %d outside [-%d, %d]",
-                      b[i], kBinCapacity, kBinCapacity);
+        if (b[i] > kBinCapacity)
+          return fail(XH_ERR_INVALID, "venv: bin value %d above the capacity %d",
+                      b[i], kBinCapacity);
     }
     HIPCHK(hipSetDevice(v->ctx->device));
     HIPCHK(copy_to_device(v->buf[which], host, bytes, v->ctx->stream));

@@ -364,12 +364,25 @@ int xh_trainer_reset_timing(xh_trainer *t);
 /* Which kernels the trainer's last rollout step and last policy epoch
  * launched, and their arithmetic, as a JSON object written NUL-terminated
  * into buf[cap]:
- *   {"rollout_step": K, "policy_train": K, "overrides": {...}}
- *   K = {"kernel": name | null (not launched yet), "math": "f32_mfma" |
- *        "bf16_split", "bf16_products_per_f32_product": p (split kernels:
- *        4 for the train epoch = 6 in layer 2 and 3 in dW2 / dH1, equal
- *        FLOPs; 6 for the rollout's layer 2), "peak_tflops": the MFMA peak of
- *        that arithmetic on MI355X (dense bf16 2500 / p, or f32 157.3)}
+ *   {"rollout_step": K, "policy_train": K, "train_grid": G,
+ *    "train_grid_cap": C, "overrides": {...}}
+ *   K = {"kernel": name | null (not launched yet),
+ *        "math": one of
+ *          "f32_mfma"             f32-input MFMA / f32 VALU: peak 157.3
+ *          "bf16_split"           bf16 MFMA on exact three-part splits: 4
+ *                                 products per f32 product in the train epoch
+ *                                 (variant library only): peak 2500 / 4
+ *          "f16_pair"             the split rollouts' layer 2 on scaled f16
+ *                                 pairs, 3 products per f32 product: 2500 / 3
+ *          "f16_pair_bf16_split"  the train epochs: layer 2 three f16
+ *                                 products, dH1 two, dW2 three bf16 (8 per 3
+ *                                 f32 products, equal FLOPs): 2500 / (8/3),
+ *        "products_per_f32_product": p (null for f32_mfma),
+ *        "bf16_products_per_f32_product": p for "bf16_split", else null,
+ *        "peak_tflops": the dense MFMA peak of that arithmetic on MI355X
+ *        (2500 / p, or 157.3)}
+ *   G = the train grid (workgroups, = gradient slabs), C = xh_config
+ *   train_grid_cap.
  * "overrides" lists the diagnostic environment variables that steer kernel
  * selection (XH_TRAIN_KERNEL, XH_ROLLOUT_KERNEL) with their values, or null
  * when unset. */

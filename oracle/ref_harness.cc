@@ -27,7 +27,21 @@
 // produces bit-identical trajectories and RNG consumption to bp::environment,
 // and that gen_env<64,2> / gen_env<128,2> reproduce it on any 8 of their bins
 // (envcheck_injected).  D = 1 and D = 3 have no reference env to compare with.
+//
+// XH_REF_BP64 (oracle/Makefile, ref_harness_bp64): the same harness compiled
+// against a copy of the reference's apps/bin_packing/bin_packing.h whose only
+// change is num_bins (:12) = 64, generated in a scratch directory of the
+// build and deleted after it (never committed, never shipped).  Its learn /
+// bench modes at B = 64, D = 2 then drive the reference's own bp::environment
+// and bp::agent -- BASELINE config 3's env pinned by the reference's code,
+// not by gen_env.  Only those modes exist in that build.
+#ifndef XH_REF_BP64
+#define XH_REF_BP64 0
+#endif
 #include <apps/bin_packing/bin_packing.h>  // pulls xylo/nn.h, rl.h, policy_gradient.h
+#if XH_REF_BP64
+static_assert(bp::num_bins == 64, "ref_harness_bp64: bin_packing.h copy with num_bins = 64");
+#endif
 
 #include <xeno/sys/file_descriptor.h>
 
@@ -35,6 +49,7 @@
 // (firstfit_agent.cc:10-28, bestfit_agent.cc:10-30, minwaste_agent.cc:10-39),
 // compiled from those files where they lie; their main() is renamed and never
 // called (mode=heuristic drives the policies with a seeded engine instead).
+#if !XH_REF_BP64
 namespace ref_firstfit {
 #define main firstfit_main
 #include <apps/bin_packing/firstfit_agent.cc>
@@ -50,6 +65,7 @@ namespace ref_minwaste {
 #include <apps/bin_packing/minwaste_agent.cc>
 #undef main
 }  // namespace ref_minwaste
+#endif
 
 #include <algorithm>
 #include <array>
@@ -350,6 +366,7 @@ void build_full(xylo::model &m, int in, const std::vector<int> &widths, int out,
     m.add_layer(std::make_unique<xylo::softmax_cross_entropy_layer>());
 }
 
+#if !XH_REF_BP64
 // ------------------------------------------------------------ mode: rng ----
 int mode_rng(std::map<std::string, std::string> &a) {
   recorder rec(a["out"]);
@@ -706,6 +723,8 @@ int mode_heuristic(std::map<std::string, std::string> &a) {
   return 0;
 }
 
+#endif  // !XH_REF_BP64
+
 // ------------------------------------------------------- mode: learn -------
 struct learn_cfg {
   std::string algo;  // ppo | klppo | ac | pg
@@ -718,10 +737,120 @@ struct learn_cfg {
   std::string opt_pi = "sgd", opt_v = "sgd";  // sgd | momentum | adam
 };
 
-template <std::size_t B, std::size_t D>
-int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
+// The env / agent / observation types a learner run drives: the reference's
+// own bp::environment / bp::agent where the shape is theirs (D = 2 and B =
+// bp::num_bins: 8 in the plain build, 64 in the XH_REF_BP64 build), gen_env
+// for every other shape.
+template <std::size_t B, std::size_t D> struct gen_world {
   using A = xylo::discrete_action<B>;
   using S = gen_obs<B, D>;
+  using env = gen_env<B, D>;
+  using agent = gen_agent<B, D>;
+  static constexpr bool real_env = false;
+  static void bins_of(const S &s, std::vector<int32_t> &out) {
+    for (auto &b : s.bins) out.insert(out.end(), b.begin(), b.end());
+  }
+  static void item_of(const S &s, std::vector<int32_t> &out) {
+    out.insert(out.end(), s.item.begin(), s.item.end());
+  }
+};
+
+// bp::environment with the per-apply log the golden's step records come from
+// (the env's own apply runs unchanged).
+class logged_bp_env : public bp::environment {
+public:
+  logged_bp_env(int index, std::vector<step_log> *log)
+      : index_(index), log_(log) {}
+  void apply(const bp::action &a, std::size_t id) override {
+    if (log_) {
+      step_log l;
+      l.env = index_;
+      l.step = steps_;
+      const bp::observation s = view(id);
+      for (auto &b : s.bins) {
+        l.bins.push_back(b.first);
+        l.bins.push_back(b.second);
+      }
+      l.item = {s.item.first, s.item.second};
+      l.choice = a.choice;
+      if (a.distrib) l.distrib = to_std(*a.distrib);
+      l.done = 0;
+      log_->push_back(l);
+    }
+    ++steps_;
+    bp::environment::apply(a, id);
+    if (log_)
+      for (auto &b : view(id).bins)
+        if (b.first < 0 || b.second < 0) log_->back().done = 1;
+  }
+
+private:
+  int index_;
+  int steps_ = 0;
+  std::vector<step_log> *log_;
+};
+
+struct bp_world {
+  using A = bp::action;
+  using S = bp::observation;
+  using env = logged_bp_env;
+  using agent = bp::agent;
+  static constexpr bool real_env = true;
+  static void bins_of(const S &s, std::vector<int32_t> &out) {
+    for (auto &b : s.bins) {
+      out.push_back(b.first);
+      out.push_back(b.second);
+    }
+  }
+  static void item_of(const S &s, std::vector<int32_t> &out) {
+    out.push_back(s.item.first);
+    out.push_back(s.item.second);
+  }
+};
+
+// The replay buffer's trajectory list (rl.h:213-296) replayed from the apply
+// log: a trajectory opens at an env's first step and after each game over,
+// forget() drops the frozen ones and keeps the open ones from their last
+// state.  Gives each learner row its (env, step) when the observation type
+// carries no tags (bp::observation).
+struct traj_book {
+  struct entry {
+    int env, start, n;
+    bool frozen;
+  };
+  std::vector<entry> list;
+  std::vector<int> open;
+  explicit traj_book(int n_env) : open(n_env, -1) {}
+  void on_apply(const step_log &l) {
+    int &o = open[l.env];
+    if (o < 0) {
+      list.push_back({l.env, l.step, 0, false});
+      o = (int)list.size() - 1;
+    }
+    ++list[o].n;
+    if (l.done) {
+      list[o].frozen = true;
+      o = -1;
+    }
+  }
+  void forget() {
+    std::vector<entry> keep;
+    std::fill(open.begin(), open.end(), -1);
+    for (auto e : list) {
+      if (e.frozen) continue;
+      e.start += e.n;
+      e.n = 0;
+      open[e.env] = (int)keep.size();
+      keep.push_back(e);
+    }
+    list = std::move(keep);
+  }
+};
+
+template <class W, std::size_t B, std::size_t D>
+int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
+  using A = typename W::A;
+  using S = typename W::S;
   auto &g = xylo::default_generator();
   g.seed(c.seed);
   const int f0 = 2 * D;
@@ -745,15 +874,20 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     if (!pg) rec->f32("init_value", to_std(val.parameters()));
   }
   const uint32_t x0 = engine_state();
-  if (rec) rec->u32("x0", {x0});
+  if (rec) {
+    rec->u32("x0", {x0});
+    // 1: the reference's own bp::environment / bp::agent drove this run
+    rec->i32("env_is_reference", {W::real_env ? 1 : 0});
+  }
 
   std::vector<step_log> log;
-  std::vector<gen_env<B, D>> envs;
+  std::vector<typename W::env> envs;
   envs.reserve(c.N);
   for (int i = 0; i < c.N; ++i) envs.emplace_back(i, rec ? &log : nullptr);
+  traj_book book(c.N);
   xylo::replay_buffer<A, S> rb;
   xylo::policy_gradient_policy<A, S> policy(pol);
-  std::vector<gen_agent<B, D>> agents;
+  std::vector<typename W::agent> agents;
   agents.reserve(c.N);
   for (int i = 0; i < c.N; ++i) agents.emplace_back(policy, envs[i], rb);
 
@@ -807,6 +941,13 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     // ---- Recorded path: the body of learn() (policy_gradient.h:159-185 /
     // 95-123), via the learners' public methods, with every intermediate.
     auto exp = rb.sample_td();
+    for (std::size_t k = log0; k < log.size(); ++k) book.on_apply(log[k]);
+    if (book.list.size() != exp.size()) {
+      std::fprintf(stderr, "traj_book: %zu trajectories, replay buffer %zu\n",
+                   book.list.size(), exp.size());
+      return 3;
+    }
+    std::size_t ti = 0;
     std::size_t ntr = 0;
     for (auto &t : exp) ntr += t.size();
     const std::size_t rows = pg ? ntr : ntr + exp.size();
@@ -816,11 +957,29 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
     std::vector<float> reward;
     std::size_t r = 0;
     for (auto &traj : exp) {
+      const traj_book::entry &be = book.list[ti++];
+      if ((std::size_t)be.n != traj.size()) {
+        std::fprintf(stderr, "traj_book: trajectory of %d transitions, "
+                     "replay buffer %zu\n", be.n, traj.size());
+        return 3;
+      }
+      int k = 0;
       for (auto &tr : traj) {
         tr.start_state->to_vector(sm[r++]);
         actions.push_back(tr.action);
-        tag_env.push_back(tr.start_state->tag_env);
-        tag_step.push_back(tr.start_state->tag_step);
+        if constexpr (W::real_env) {
+          tag_env.push_back(be.env);
+          tag_step.push_back(be.start + k);
+        } else {
+          tag_env.push_back(tr.start_state->tag_env);
+          tag_step.push_back(tr.start_state->tag_step);
+          if (be.env != tr.start_state->tag_env ||
+              be.start + k != tr.start_state->tag_step) {
+            std::fprintf(stderr, "traj_book disagrees with the tags\n");
+            return 3;
+          }
+        }
+        ++k;
         is_end.push_back(0);
         frozen.push_back(traj.frozen());
         choice.push_back(tr.action.choice);
@@ -829,8 +988,13 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
       if (!pg) {
         actions.push_back(actions.back());
         traj.back().end_state.to_vector(sm[r++]);
-        tag_env.push_back(traj.back().end_state.tag_env);
-        tag_step.push_back(traj.back().end_state.tag_step);
+        if constexpr (W::real_env) {
+          tag_env.push_back(be.env);
+          tag_step.push_back(be.start + be.n);
+        } else {
+          tag_env.push_back(traj.back().end_state.tag_env);
+          tag_step.push_back(traj.back().end_state.tag_step);
+        }
         is_end.push_back(1);
         frozen.push_back(traj.frozen());
         choice.push_back(actions.back().choice);
@@ -891,13 +1055,14 @@ int run_learn(learn_cfg c, recorder *rec, double *steps_per_s) {
               log_pi->grads.empty() ? 0 : log_pi->grads[0].size()});
     rec->f32(p + "policy_params", to_std(pol.parameters()));
     rb.forget();
+    book.forget();
     rec->u32(p + "x_end", {engine_state()});
     {
       std::vector<int32_t> fb, fi;
       for (auto &e : envs) {
         S s = e.view(0);
-        for (auto &b : s.bins) fb.insert(fb.end(), b.begin(), b.end());
-        fi.insert(fi.end(), s.item.begin(), s.item.end());
+        W::bins_of(s, fb);
+        W::item_of(s, fi);
       }
       rec->i32(p + "final_bins", fb, {(uint64_t)c.N, B, D});
       rec->i32(p + "final_item", fi, {(uint64_t)c.N, D});
@@ -933,13 +1098,16 @@ int mode_learn(std::map<std::string, std::string> &a, bool bench) {
   if (!bench) rec = std::make_unique<recorder>(a["out"]);
   c.record = !bench;
   recorder *r = rec.get();
+  if (B == (int)bp::num_bins && D == 2)
+    return run_learn<bp_world, bp::num_bins, 2>(c, r, nullptr);
 #define XH_CASE(b, d)                                                          \
-  if (B == b && D == d) return run_learn<b, d>(c, r, nullptr);
-  XH_CASE(8, 2)
+  if (B == b && D == d) return run_learn<gen_world<b, d>, b, d>(c, r, nullptr);
   XH_CASE(8, 1)
   XH_CASE(16, 2)
   XH_CASE(32, 1)
+#if !XH_REF_BP64
   XH_CASE(64, 2)
+#endif
   XH_CASE(128, 3)
 #undef XH_CASE
   std::fprintf(stderr, "unsupported B=%d D=%d\n", B, D);
@@ -956,12 +1124,14 @@ int main(int argc, char **argv) {
   }
   auto a = parse_args(argc, argv);
   std::string mode = argv[1];
+#if !XH_REF_BP64
   if (mode == "rng") return mode_rng(a);
   if (mode == "envcheck") return mode_envcheck(a);
   if (mode == "deep") return mode_deep(a);
   if (mode == "driver") return mode_driver(a);
   if (mode == "random") return mode_random(a);
   if (mode == "heuristic") return mode_heuristic(a);
+#endif
   if (mode == "learn") return mode_learn(a, false);
   if (mode == "bench") return mode_learn(a, true);
   std::fprintf(stderr, "unknown mode %s\n", mode.c_str());

@@ -21,6 +21,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+# the same harness compiled against the reference's bin_packing.h with
+# num_bins = 64 (oracle/Makefile): the config-3 shape on bp::environment
+HARNESS_BP64 = os.path.join(REPO, "oracle", "_ref", "ref_harness_bp64")
+BP64 = ("ppo_b64d2", "ppo_b64d2_n160")
 REF = "/root/reference"
 
 _DT = {b"f": np.float32, b"d": np.float64, b"i": np.int32, b"u": np.uint32}
@@ -68,7 +72,8 @@ FIXTURES = {
     # BASELINE config 2 shape (1-D, 32 bins, [64,64])
     "ppo_b32d1": ("learn", ["algo=ppo", "B=32", "D=1", "widths=64,64", "N=6",
                             "T=4", "iters=2", "seed=5"]),
-    # BASELINE config 3/4 shape (2-D, 64 bins, [128,128])
+    # BASELINE config 3/4 shape (2-D, 64 bins, [128,128]) on the reference's
+    # own bp::environment / bp::agent at 64 bins (ref_harness_bp64)
     "ppo_b64d2": ("learn", ["algo=ppo", "B=64", "D=2", "widths=128,128",
                             "N=4", "T=4", "iters=2", "seed=11"]),
     # the config-3 shape with enough envs for several 64-row groups per train
@@ -137,20 +142,28 @@ FIXTURES = {
 
 
 def main(names):
-    if not os.path.exists(HARNESS):
-        sys.exit("build the harness first: make -C oracle ref")
+    if not (os.path.exists(HARNESS) and os.path.exists(HARNESS_BP64)):
+        sys.exit("build the harnesses first: make -C oracle ref")
     names = names or list(FIXTURES)
     for name in names:
         mode, args = FIXTURES[name][:2]
         drop = FIXTURES[name][2] if len(FIXTURES[name]) > 2 else ()
         with tempfile.TemporaryDirectory() as td:
             rec = os.path.join(td, "out.rec")
-            subprocess.run([HARNESS, mode, "out=" + rec] + args, check=True,
+            harness = HARNESS_BP64 if name in BP64 else HARNESS
+            subprocess.run([harness, mode, "out=" + rec] + args, check=True,
                            cwd=td)
             arrs = read_records(rec)
             arrs = {k: v for k, v in arrs.items()
                     if not any(k.endswith(d) for d in drop)}
         meta = {"mode": mode, "args": " ".join(args)}
+        if "env_is_reference" in arrs:
+            # which environment the reference learner drove (ref_harness.cc)
+            kv = dict(a.split("=", 1) for a in args)
+            meta["env"] = ("bp::environment (apps/bin_packing/bin_packing.h%s)"
+                           % (", num_bins = 64" if name in BP64 else "")
+                           if arrs["env_is_reference"][0] else
+                           "gen_env<%s,%s> (ref_harness.cc)" % (kv["B"], kv["D"]))
         for k, v in meta.items():
             arrs["meta_" + k] = np.array(v)
         path = os.path.join(HERE, name + ".npz")

@@ -43,32 +43,89 @@ def test_learn_refuses_items_outside_the_item_table(ctx):
 
 
 def test_state_setters_reject_out_of_range_bins(ctx):
-    """Bin values outside [-capacity, capacity] are refused by
-    set_env_state, set_buffer(BINS) and the venv's BINS.  Negative values
-    down to -capacity stay legal: they are the overflowed (game-over) states
-    an apply by hand leaves (bin_packing.h:53-63), which the drop-in layer
-    uploads (tests/compat/bound_env_by_hand.cc)."""
+    """Bin values above the capacity are refused by set_env_state,
+    set_buffer(BINS) and the venv's BINS.  Every negative int8 value stays
+    legal: an apply by hand past game over keeps subtracting
+    (bin_packing.h:53-63), so -4, -8, -12, ... are reachable states the
+    drop-in layer uploads (tests/compat/bound_env_by_hand.cc)."""
     from dependence_free_rl_amd import VecEnv, XhError
     from dependence_free_rl_amd.trainer import BUF_BINS
     tr = _trainer(ctx)
     bins, items = tr.env_state(0, 2)
     bad = bins.copy()
-    bad[1, 3, 0] = -9
-    with pytest.raises(XhError, match="outside"):
+    bad[1, 3, 0] = 9
+    with pytest.raises(XhError, match="above the capacity"):
         tr.set_env_state(0, bad, items)
-    bad[1, 3, 0] = -3  # an overflowed bin: accepted
+    bad[1, 3, 0] = -12  # overflowed twice: accepted
     tr.set_env_state(0, bad, items)
     b = tr.buffer(BUF_BINS).copy()
     b[0, 0, 0, 1] = 9
-    with pytest.raises(XhError, match="outside"):
+    with pytest.raises(XhError, match="above the capacity"):
         tr.set_buffer(BUF_BINS, b)
+    b[0, 0, 0, 1] = -100
+    tr.set_buffer(BUF_BINS, b)
     tr.close()
     env = VecEnv(ctx, num_envs=8, bins=8, dims=2, rng_state=1)
     vb, _ = env.view()
-    vb[2, 1, 1] = -100
-    with pytest.raises(XhError, match="outside"):
+    vb[2, 1, 1] = 10
+    with pytest.raises(XhError, match="above the capacity"):
         env.set(3, vb)  # VENV_BINS
+    vb[2, 1, 1] = -100
+    env.set(3, vb)
     env.close()
+
+
+@pytest.mark.parametrize("B,D,algo", [(64, 2, "ppo"), (128, 3, "ac")])
+def test_overflowed_start_states_run_the_f32_kernels(ctx, monkeypatch, B, D,
+                                                     algo):
+    """A start state with a bin below -capacity (|bins / capacity| > 1, beyond
+    the f16-pair kernels' H1 bound) is rolled out and
+    learned by the f32-MFMA kernels: the iteration equals, bit for bit, the
+    same iteration run with XH_TRAIN_KERNEL=f32 XH_ROLLOUT_KERNEL=f32, and the
+    next iteration (states >= 0 again) is back on the f16-pair kernels."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS,
+                                                BUF_POLICY_GRADS, BUF_PROBS)
+    # T = 1: the whole batch is the overflowed slot 0
+    N, T, widths = 16, 1, (128, 128)
+    pp, vp = init_policy(D, *widths, seed=5), init_value(B, D, seed=6)
+
+    def run(f32):
+        if f32:
+            monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
+            monkeypatch.setenv("XH_ROLLOUT_KERNEL", "f32")
+        else:
+            monkeypatch.delenv("XH_TRAIN_KERNEL", raising=False)
+            monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
+        tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
+                     widths=widths, rng_state=77)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        bins, items = tr.env_state()
+        bins[3, 7, 0] = -20   # overflowed (game over) start states
+        bins[9, 0, :] = -128
+        tr.set_env_state(0, bins, items)
+        tr.rollout()
+        tr.learn()
+        out = {b: tr.buffer(b).copy()
+               for b in (BUF_ACTION, BUF_BINS, BUF_POLICY_GRADS, BUF_PROBS)}
+        out["params"] = tr.params(POLICY)
+        out["kinfo"] = tr.kernel_info()
+        tr.rollout()
+        tr.learn()
+        out["kinfo2"] = tr.kernel_info()
+        tr.close()
+        return out
+
+    wide, ref = run(False), run(True)
+    f32_train = "policy_train8_kernel"
+    assert wide["kinfo"]["policy_train"]["kernel"] == f32_train, wide["kinfo"]
+    assert wide["kinfo2"]["policy_train"]["kernel"] != f32_train, wide["kinfo2"]
+    assert wide["kinfo2"]["policy_train"]["math"] == "f16_pair_bf16_split"
+    assert (wide[BUF_BINS][0] < -8).any()
+    for k in (BUF_ACTION, BUF_BINS, BUF_POLICY_GRADS, BUF_PROBS, "params"):
+        np.testing.assert_array_equal(wide[k], ref[k], err_msg=str(k))
+    assert np.isfinite(wide["params"]).all()
 
 
 def test_env_overrides_of_many_envs(ctx):

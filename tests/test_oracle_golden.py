@@ -267,3 +267,23 @@ def test_venv_driver_matches_reference():
     for k in ("bins", "item", "reward", "done"):
         np.testing.assert_array_equal(part[k], full[k][:, 5:9])
     assert part["x_end"] == full["x_end"]
+
+
+def test_reference_env_pins_the_d2_goldens():
+    """Every learner golden of a D = 2 shape the reference's env can take was
+    driven by the reference's own bp::environment / bp::agent: 8 bins from
+    apps/bin_packing/bin_packing.h as it is, BASELINE config 3's 64 bins from
+    the same header compiled with num_bins = 64 (oracle/Makefile,
+    ref_harness_bp64).  The other shapes (1-D, 3-D, 32 / 128 bins) are
+    gen_env's and say so."""
+    for name in ("ppo_b64d2", "ppo_b64d2_n160"):
+        g = golden(name)
+        assert int(g["env_is_reference"][0]) == 1, name
+        assert "bp::environment" in str(g["meta_env"]), name
+        assert "num_bins = 64" in str(g["meta_env"]), name
+    for name in ("ppo_b8d2", "ac_b8d2", "klppo_b8d2", "ppo_adam_b8d2",
+                 "ac_mom_b8d2", "pg_b8d2"):
+        assert int(golden(name)["env_is_reference"][0]) == 1, name
+    for name in ("ppo_b32d1", "ac_b128d3", "pg_b8d1"):
+        g = golden(name)
+        assert int(g["env_is_reference"][0]) == 0 and "gen_env" in str(g["meta_env"])
