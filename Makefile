@@ -14,14 +14,15 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8x_kernels.o \
-            $(SRC)/policy_split4h_kernels.o \
-            $(SRC)/train_select.o $(SRC)/xylo_hip.o
+            $(SRC)/policy_split4h_kernels.o $(SRC)/loss_kernels.o \
+            $(SRC)/train_select.o $(SRC)/model_api.o $(SRC)/xylo_hip.o
 # superseded train kernels (the config-3 / config-5
 # epoch's earlier forms), kept for A/B runs in the variant library only
 VARIANT_KERNELS := policy_split_kernels policy_split128_kernels \
             policy_split8w_kernels policy_split8wp_kernels \
             policy_split4p_kernels policy_split8wg_kernels
-HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h include/xylo_hip.h
+HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h \
+            $(SRC)/xh_host.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
 # apps/bin_packing drivers (when the reference tree is present) and our own
@@ -65,6 +66,9 @@ $(SRC)/xylo_hip.o: $(SRC)/xylo_hip.cpp $(HDRS)
 $(SRC)/train_select.o: $(SRC)/train_select.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(SRC)/model_api.o: $(SRC)/model_api.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 # the variant library: the product objects + the superseded train kernels,
 # with the dispatch that reaches them (XH_TRAIN_KERNEL=split4w / split8w /
 # split8wp / split4p / split8wg / split128); loaded through XH_LIB_PATH only
@@ -100,7 +104,8 @@ oracle:
 
 # test programs of the drop-in layer (tests/compat), prebuilt so the GPU box
 # runs them without a compiler step
-COMPAT_TESTS := $(COMPAT)/bound_env_by_hand $(COMPAT)/save_weights
+COMPAT_TESTS := $(COMPAT)/bound_env_by_hand $(COMPAT)/save_weights \
+                $(COMPAT)/composed_learner
 
 compat: $(EXAMPLES) $(COMPAT_TESTS)
 	@mkdir -p $(COMPAT)
@@ -115,6 +120,10 @@ $(COMPAT)/bound_env_by_hand: tests/compat/bound_env_by_hand.cc $(COMPAT_HDRS) $(
 	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
 
 $(COMPAT)/save_weights: tests/compat/save_weights.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
+
+$(COMPAT)/composed_learner: tests/compat/composed_learner.cc $(COMPAT_HDRS) $(LIB)
 	@mkdir -p $(COMPAT)
 	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
 

@@ -40,7 +40,8 @@ class Config(C.Structure):
         ("lambda_", C.c_float), ("clip_eps", C.c_float),
         ("rng_state", C.c_uint32), ("kl_beta", C.c_float),
         ("kl_target", C.c_float), ("adv_normalize", C.c_int),
-        ("lr_scale_rows", C.c_int), ("train_grid_cap", C.c_int)]
+        ("lr_scale_rows", C.c_int), ("train_grid_cap", C.c_int),
+        ("record_distrib", C.c_int)]
 
 
 class Eval(C.Structure):
@@ -112,6 +113,16 @@ def _load():
         "xh_venv_synchronize": (i, [vp]),
         "xh_model_eval": (i, [vp, vp, i, vp, sz, vp, i, i, vp, sz,
                               C.POINTER(C.c_int)]),
+        "xh_model_forward": (i, [vp, vp, i, vp, sz, vp, i, i, vp, sz,
+                                 C.POINTER(C.c_int)]),
+        "xh_model_gradient": (i, [vp, vp, i, vp, sz, vp, i, i, vp, i, vp]),
+        "xh_layer_backward": (i, [vp, vp, vp, sz, vp, i, i, vp, i, vp]),
+        "xh_layer_gradient": (i, [vp, vp, vp, i, i, vp, i, vp, sz]),
+        "xh_action_loss_grad": (i, [vp, i, i, i, vp, vp, vp, vp, C.c_float,
+                                    vp]),
+        "xh_optimizer_apply": (i, [vp, i, C.c_float, C.c_float, C.c_float,
+                                   C.c_float, C.c_float, vp, vp, vp, vp, sz]),
+        "xh_trainer_forget": (i, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -126,6 +137,8 @@ class Layer(C.Structure):
 
 
 LAYER_FULL, LAYER_CONV1D_1, LAYER_RELU, LAYER_SOFTMAX, LAYER_SOFTMAX_XENT = range(5)
+(LOSS_GRADIENT_LOG, LOSS_SOFTMAX_GRADIENT_LOG, LOSS_CLIPPED,
+ LOSS_KL_REGULATED) = range(4)
 
 lib = _load()
 for _name, _mirror in (("xh_config", Config), ("xh_eval", Eval),

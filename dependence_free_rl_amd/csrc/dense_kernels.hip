@@ -538,4 +538,134 @@ hipError_t model_forward(const ModelLayer *layers, int nl, const float *params,
   return e;
 }
 
+// ------------------------------------- one layer: forward / backward / grad --
+// The reference's layer interface (nn.h:20-33) on the device, one layer at a
+// time, for model::forward / model::gradient / optimizer::step of the drop-in
+// layer (xh_model_forward, xh_model_gradient, xh_layer_backward,
+// xh_layer_gradient).  Dense layers (full: nn.h:71-100; conv1d_1: the same
+// Dense over rows * points, nn.h:127-186) run on the f32 MFMA GEMM above.
+struct EpStore {  // Y[m][n] = c
+  float *y;
+  int ld;
+  __device__ void operator()(int m, int n, int, float c) const {
+    y[(size_t)m * ld + n] = c;
+  }
+};
+
+// relu_activation::backward (nn.h:363-376): the input's sign gates backprop
+__global__ void relu_backward_kernel(const float *x, const float *bp, float *out,
+                                     long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    out[i] = x[i] > 0.0f ? bp[i] : 0.0f;
+}
+
+// softmax_layer::backward (nn.h:393-417): the row's softmax s (the forward's
+// exp / sum, no max shift) and the Jacobian product (diag(s) - s s^T) g,
+// evaluated as s_j g_j - s_j (s . g) (the same sum, one rounding per term
+// instead of a B x B matrix).  One thread per row.
+__global__ void softmax_backward_kernel(const float *x, const float *bp,
+                                        float *out, int rows, int cols) {
+#pragma clang fp contract(off)
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += gridDim.x * blockDim.x) {
+    const float *xr = x + (size_t)r * cols, *g = bp + (size_t)r * cols;
+    float *o = out + (size_t)r * cols;
+    float sum = 0.0f;
+    for (int c = 0; c < cols; ++c) sum += expf(xr[c]);
+    float dot = 0.0f;
+    for (int c = 0; c < cols; ++c) dot += (expf(xr[c]) / sum) * g[c];
+    for (int c = 0; c < cols; ++c) {
+      const float sj = expf(xr[c]) / sum;
+      o[c] = sj * g[c] - sj * dot;
+    }
+  }
+}
+
+static unsigned elem_blocks(long n) {
+  const long b = (n + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
+// points of a Dense layer's input row (1 for full_layer)
+static int layer_points(const ModelLayer &L, int cols) {
+  return L.kind == kLayerFull ? 1 : cols / L.in;
+}
+
+hipError_t layer_forward(const ModelLayer &L, const float *W, const float *x,
+                         int rows, int cols, float *y, hipStream_t s) {
+  using namespace dense;
+  const long n = (long)rows * cols;
+  switch (L.kind) {
+    case kLayerFull:
+    case kLayerConv1d: {
+      const int M = rows * layer_points(L, cols);
+      EpBiasAct ep{y, L.out, W + (size_t)L.out * L.in, 0};
+      return gemm(RowMajor{x, L.in}, RowMajor{W, L.in}, ep, M, L.out, L.in,
+                  nullptr, 0, 1, s);
+    }
+    case kLayerRelu: {
+      hipError_t e = hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(relu_kernel, dim3(elem_blocks(n)), dim3(256), 0, s, y, n);
+      return hipGetLastError();
+    }
+    default: {  // softmax / softmax_cross_entropy: the same forward
+      hipError_t e = hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(softmax_rows_kernel, dim3((rows + 255) / 256),
+                         dim3(256), 0, s, y, rows, cols);
+      return hipGetLastError();
+    }
+  }
+}
+
+hipError_t layer_backward(const ModelLayer &L, const float *W, const float *x,
+                          int rows, int cols, const float *bp, float *out,
+                          hipStream_t s) {
+  using namespace dense;
+  const long n = (long)rows * cols;
+  switch (L.kind) {
+    case kLayerFull:
+    case kLayerConv1d: {  // dX = dY W (nn.h:77-79, 149-162)
+      const int M = rows * layer_points(L, cols);
+      return gemm(RowMajor{bp, L.out}, ColMajor{W, L.in}, EpStore{out, L.in}, M,
+                  L.in, L.out, nullptr, 0, 1, s);
+    }
+    case kLayerRelu:
+      hipLaunchKernelGGL(relu_backward_kernel, dim3(elem_blocks(n)), dim3(256),
+                         0, s, x, bp, out, n);
+      return hipGetLastError();
+    case kLayerSoftmax:
+      hipLaunchKernelGGL(softmax_backward_kernel, dim3((rows + 255) / 256),
+                         dim3(256), 0, s, x, bp, out, rows, cols);
+      return hipGetLastError();
+    default:  // softmax_cross_entropy_layer::backward passes backprop through
+      return hipMemcpyAsync(out, bp, n * 4, hipMemcpyDeviceToDevice, s);
+  }
+}
+
+int layer_gradient_splits(const ModelLayer &L, int rows, int cols) {
+  if (L.kind != kLayerFull && L.kind != kLayerConv1d) return 0;
+  const long M = (long)rows * layer_points(L, cols);
+  const long sp = (M + 1023) / 1024;
+  return (int)(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
+}
+
+hipError_t layer_gradient(const ModelLayer &L, const float *x, int rows,
+                          int cols, const float *bp, float *slab, int stride,
+                          float *grad, hipStream_t s) {
+  using namespace dense;
+  if (L.kind != kLayerFull && L.kind != kLayerConv1d) return hipSuccess;
+  // [dW | db] = dY^T [X | 1] over rows * points (nn.h:81-100, 164-186),
+  // split-K over the rows into slabs, then the fixed-order slab sum
+  const int M = rows * layer_points(L, cols);
+  const int splits = layer_gradient_splits(L, rows, cols);
+  EpSlab es{slab, stride, 0, L.out * L.in, L.in};
+  hipError_t e = gemm(ColMajor{bp, L.out}, RowsOnes{x, L.in, L.in}, es, L.out,
+                      L.in + 1, M, nullptr, 0, splits, s);
+  if (e != hipSuccess) return e;
+  return launch_slab_reduce(slab, splits, stride, L.out * L.in + L.out, grad, s);
+}
+
 }  // namespace xh

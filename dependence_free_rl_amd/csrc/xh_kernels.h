@@ -205,6 +205,27 @@ struct ModelLayer {
 hipError_t model_forward(const ModelLayer *layers, int nl, const float *params,
                          const float *x, int rows, int cols, float *a, float *b,
                          const float **out, int *out_cols, hipStream_t s);
+// One layer of the reference's layer interface (nn.h:20-33) on device
+// buffers: forward (y: rows x output width), backward (out: rows x cols, the
+// data gradient), gradient (grad: the layer's flat parameter gradient, via
+// layer_gradient_splits(...) slabs of `stride` floats; activations: none).
+hipError_t layer_forward(const ModelLayer &L, const float *W, const float *x,
+                         int rows, int cols, float *y, hipStream_t s);
+hipError_t layer_backward(const ModelLayer &L, const float *W, const float *x,
+                          int rows, int cols, const float *bp, float *out,
+                          hipStream_t s);
+int layer_gradient_splits(const ModelLayer &L, int rows, int cols);
+hipError_t layer_gradient(const ModelLayer &L, const float *x, int rows,
+                          int cols, const float *bp, float *slab, int stride,
+                          float *grad, hipStream_t s);
+// The discrete-action loss gradients of a batch (rl.h:33-74 row by row;
+// policy_gradient.h:24-85): out [rows][range].
+enum LossKind { kLossGradientLog = 0, kLossSoftmaxGradientLog = 1,
+                kLossClipped = 2, kLossKlRegulated = 3 };
+hipError_t launch_action_loss(int kind, int rows, int range,
+                              const int32_t *choice, const float *distrib,
+                              const float *adv, const float *probs, float param,
+                              float *out, hipStream_t s);
 
 // REINFORCE (pg_kernels.hip).  Batch.T = the per-iteration step bound.
 struct PgStepArgs {

@@ -24,55 +24,12 @@
 #include <vector>
 
 #include "../../include/xylo_hip.h"
+#include "xh_host.h"
 #include "xh_kernels.h"
 
+using namespace xh::host;
+
 namespace {
-
-thread_local std::string g_err;
-
-int fail(int code, const char *fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  std::vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-
-#define HIPCHK(x)                                                         \
-  do {                                                                    \
-    hipError_t e_ = (x);                                                  \
-    if (e_ != hipSuccess)                                                 \
-      return fail(XH_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #x,     \
-                  hipGetErrorString(e_));                                 \
-  } while (0)
-
-#define RCCLCHK(x)                                                        \
-  do {                                                                    \
-    ncclResult_t r_ = (x);                                                \
-    if (r_ != ncclSuccess)                                                \
-      return fail(XH_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #x,    \
-                  ncclGetErrorString(r_));                                \
-  } while (0)
-
-#define CHK(x)                   \
-  do {                           \
-    int s_ = (x);                \
-    if (s_ != XH_OK) return s_;  \
-  } while (0)
-
-// No exception may cross the ABI.
-template <class F>
-int guard(F &&f) {
-  try {
-    return f();
-  } catch (const std::exception &e) {
-    return fail(XH_ERR_INVALID, "exception: %s", e.what());
-  } catch (...) {
-    return fail(XH_ERR_INVALID, "unknown exception");
-  }
-}
 
 uint32_t mstd_pow(uint64_t k) {  // 16807^k mod (2^31-1)
   uint64_t acc = 1, base = 16807;
@@ -85,15 +42,6 @@ uint32_t mstd_pow(uint64_t k) {  // 16807^k mod (2^31-1)
 }
 
 }  // namespace
-
-struct xh_ctx {
-  int device = 0, rank = 0, world = 1;
-  hipStream_t stream = nullptr;
-  ncclComm_t comm = nullptr;
-  int trainers = 0;      // live trainers on this context
-  bool closing = false;  // xh_ctx_destroy called while trainers were alive
-  int fault = 0;         // xh_ctx_inject_fault (test hook): pending fault
-};
 
 namespace {
 void ctx_free(xh_ctx *c) {
@@ -373,27 +321,6 @@ void *buffer_ptr(const xh_trainer *t, int which) {
     case XH_BUF_LEN: return t->pg.len;
   }
   return nullptr;
-}
-
-// Copies between the device and caller (pageable) host memory, ordered on
-// the trainer's stream and waited for before returning (the caller may free
-// or read its buffer right after).  Not hipMemcpy: the trainer's stream is
-// non-blocking, so a null-stream H2D copy of pageable memory, which returns
-// once the bytes are staged, is not ordered before the next kernel on it --
-// measured: parameters read stale by the first rollout kernel, intermittently.
-hipError_t copy_to_host(void *host, const void *dev, size_t n, hipStream_t s) {
-  const hipError_t e = hipMemcpyAsync(host, dev, n, hipMemcpyDeviceToHost, s);
-  return e != hipSuccess ? e : hipStreamSynchronize(s);
-}
-hipError_t copy_to_device(void *dev, const void *host, size_t n,
-                          hipStream_t s) {
-  const hipError_t e = hipMemcpyAsync(dev, host, n, hipMemcpyHostToDevice, s);
-  return e != hipSuccess ? e : hipStreamSynchronize(s);
-}
-
-int copy_ok(hipError_t e) {
-  return e == hipSuccess ? XH_OK
-                         : fail(XH_ERR_HIP, "copy: %s", hipGetErrorString(e));
 }
 
 constexpr uint64_t kEvalStride = 1ull << 26;  // draws between env streams
@@ -1544,8 +1471,9 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
       A(&t->adv_part, (size_t)xh::gae_grid((int)N) * 2 * 8);
       A(&t->adv_stats, 2 * 8);
     }
-    if (c.algo == XH_KLPPO) {
+    if (c.algo == XH_KLPPO || c.record_distrib)
       A(&t->qold, T * N * c.bins * 4);
+    if (c.algo == XH_KLPPO) {
       A(&t->beta, 4);
       A(&t->kl_log, (size_t)c.epochs * 3 * 4);
       A(&t->kl_part, (size_t)t->pslab_n * 8);
@@ -1703,6 +1631,14 @@ int xh_trainer_learn(xh_trainer *t) {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
     HIPCHK(hipSetDevice(t->ctx->device));
     return do_learn(t);
+  });
+}
+
+int xh_trainer_forget(xh_trainer *t) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    t->need_shift = true;  // as at the end of do_learn / do_pg_learn
+    return XH_OK;
   });
 }
 
@@ -2029,73 +1965,6 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
       t->env_override[first + e] = std::move(v);
     }
     return XH_OK;
-  });
-}
-
-// ---------------------------------------------------------- model::eval --
-int xh_model_eval(xh_ctx *ctx, const xh_layer *layers, int nlayers,
-                  const float *params, size_t nparams, const float *x,
-                  int rows, int cols, float *out, size_t out_cap,
-                  int *out_cols) {
-  return guard([&]() -> int {
-    if (!ctx || !layers || nlayers < 1 || !params || !x || !out || !out_cols)
-      return fail(XH_ERR_INVALID, "model_eval: null arg");
-    if (rows < 1 || cols < 1)
-      return fail(XH_ERR_INVALID, "model_eval: %d x %d input", rows, cols);
-    std::vector<xh::ModelLayer> ml((size_t)nlayers);
-    size_t np = 0, widest = (size_t)cols;
-    int c = cols;
-    for (int l = 0; l < nlayers; ++l) {
-      const xh_layer &L = layers[l];
-      ml[l] = xh::ModelLayer{L.kind, L.in, L.out};
-      switch (L.kind) {
-        case XH_LAYER_FULL:
-        case XH_LAYER_CONV1D_1:
-          if (L.in < 1 || L.out < 1 ||
-              (L.kind == XH_LAYER_FULL ? c != L.in : c % L.in != 0))
-            return fail(XH_ERR_INVALID, "model_eval: layer %d (%d -> %d) on "
-                        "%d features", l, L.in, L.out, c);
-          c = L.kind == XH_LAYER_FULL ? L.out : c / L.in * L.out;
-          np += (size_t)L.out * L.in + L.out;
-          break;
-        case XH_LAYER_RELU:
-        case XH_LAYER_SOFTMAX:
-        case XH_LAYER_SOFTMAX_XENT:
-          break;
-        default:
-          return fail(XH_ERR_INVALID, "model_eval: layer kind %d", L.kind);
-      }
-      widest = std::max(widest, (size_t)c);
-    }
-    if (np != nparams)
-      return fail(XH_ERR_INVALID, "model_eval: %zu parameters, the layers "
-                  "need %zu", nparams, np);
-    if ((size_t)rows * c > out_cap)
-      return fail(XH_ERR_INVALID, "model_eval: output needs %zu floats, "
-                  "capacity %zu", (size_t)rows * c, out_cap);
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    const size_t act = (size_t)rows * widest;
-    float *dev = nullptr;
-    HIPCHK(hipStreamSynchronize(s));
-    HIPCHK(hipMalloc((void **)&dev, sizeof(float) * (np + 3 * act)));
-    float *dp = dev, *dx = dev + np, *da = dx + act, *db = da + act;
-    int st = copy_ok(copy_to_device(dp, params, np * 4, s));
-    if (st == XH_OK)
-      st = copy_ok(copy_to_device(dx, x, (size_t)rows * cols * 4, s));
-    const float *res = nullptr;
-    int oc = 0;
-    if (st == XH_OK) {
-      const hipError_t e = xh::model_forward(ml.data(), nlayers, dp, dx, rows,
-                                             cols, da, db, &res, &oc, s);
-      if (e != hipSuccess)
-        st = fail(XH_ERR_HIP, "model_eval: %s", hipGetErrorString(e));
-    }
-    if (st == XH_OK) st = copy_ok(copy_to_host(out, res, (size_t)rows * oc * 4, s));
-    (void)hipStreamSynchronize(s);
-    (void)hipFree(dev);
-    if (st == XH_OK) *out_cols = oc;
-    return st;
   });
 }
 

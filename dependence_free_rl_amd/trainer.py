@@ -144,6 +144,124 @@ def model_eval(ctx, layers, params, x):
     return out[:rows * oc.value].reshape(rows, oc.value).copy()
 
 
+_LAYER_KINDS = {"full": _lib.LAYER_FULL, "conv1d_1": _lib.LAYER_CONV1D_1,
+                "relu": _lib.LAYER_RELU, "softmax": _lib.LAYER_SOFTMAX,
+                "softmax_xent": _lib.LAYER_SOFTMAX_XENT}
+
+
+def _layers(layers):
+    arr = (_lib.Layer * len(layers))()
+    for i, (k, a, b) in enumerate(layers):
+        arr[i].kind, arr[i].inp, arr[i].out = _LAYER_KINDS[k], a, b
+    return arr
+
+
+def _widths(layers, cols):
+    w = [cols]
+    for k, a, b in layers:
+        w.append(b if k == "full" else w[-1] // a * b if k == "conv1d_1"
+                 else w[-1])
+    return w
+
+
+def model_forward(ctx, layers, params, x):
+    """xylo::model::forward on the device (xh_model_forward): the input and
+    every layer's output, as a list of [rows][width] arrays."""
+    x = np.ascontiguousarray(x, np.float32)
+    p = np.ascontiguousarray(params, np.float32)
+    rows, cols = x.shape
+    w = _widths(layers, cols)
+    acts = np.zeros(rows * sum(w), np.float32)
+    got = (C.c_int * (len(layers) + 1))()
+    check(_lib.lib.xh_model_forward(ctx.h, _layers(layers), len(layers),
+                                    _ptr(p), p.size, _ptr(x), rows, cols,
+                                    _ptr(acts), acts.size, got))
+    out, off = [], 0
+    for k in range(len(layers) + 1):
+        assert got[k] == w[k]
+        out.append(acts[off:off + rows * w[k]].reshape(rows, w[k]).copy())
+        off += rows * w[k]
+    return out
+
+
+def model_gradient(ctx, layers, params, inputs, target):
+    """xylo::model::gradient on the device (xh_model_gradient): inputs = the
+    first len(layers) arrays of model_forward, target = dL/d(output)."""
+    p = np.ascontiguousarray(params, np.float32)
+    rows, cols = inputs[0].shape
+    flat = np.ascontiguousarray(np.concatenate([np.ravel(a) for a in
+                                                inputs[:len(layers)]]),
+                                np.float32)
+    t = np.ascontiguousarray(target, np.float32)
+    g = np.zeros(p.size, np.float32)
+    check(_lib.lib.xh_model_gradient(ctx.h, _layers(layers), len(layers),
+                                     _ptr(p), p.size, _ptr(flat), rows, cols,
+                                     _ptr(t), t.shape[1], _ptr(g)))
+    return g
+
+
+def layer_backward(ctx, layer, params, x, backprop):
+    """layer::backward of one layer on the device (xh_layer_backward)."""
+    x = np.ascontiguousarray(x, np.float32)
+    bp = np.ascontiguousarray(backprop, np.float32)
+    p = np.ascontiguousarray(params, np.float32)
+    out = np.zeros_like(x)
+    check(_lib.lib.xh_layer_backward(ctx.h, _layers([layer]), _ptr(p), p.size,
+                                     _ptr(x), x.shape[0], x.shape[1], _ptr(bp),
+                                     bp.shape[1], _ptr(out)))
+    return out
+
+
+def layer_gradient(ctx, layer, x, backprop):
+    """layer::gradient of one layer on the device (xh_layer_gradient)."""
+    x = np.ascontiguousarray(x, np.float32)
+    bp = np.ascontiguousarray(backprop, np.float32)
+    k, a, b = layer
+    n = a * b + b if k in ("full", "conv1d_1") else 0
+    g = np.zeros(max(n, 1), np.float32)
+    check(_lib.lib.xh_layer_gradient(ctx.h, _layers([layer]), _ptr(x),
+                                     x.shape[0], x.shape[1], _ptr(bp),
+                                     bp.shape[1], _ptr(g), n))
+    return g[:n]
+
+
+LOSSES = {"gradient_log": _lib.LOSS_GRADIENT_LOG,
+          "policy_loss": _lib.LOSS_SOFTMAX_GRADIENT_LOG,
+          "surrogate_loss": _lib.LOSS_CLIPPED,
+          "kl_regulated": _lib.LOSS_KL_REGULATED}
+
+
+def action_loss_grad(ctx, kind, choice, advantage, probs, distrib=None,
+                     param=0.2):
+    """The discrete-action loss gradients of a batch (xh_action_loss_grad):
+    kind in LOSSES; probs [rows][range] (the model's output), distrib the
+    actions' sampling distributions (all kinds but policy_loss)."""
+    probs = np.ascontiguousarray(probs, np.float32)
+    rows, rng = probs.shape
+    ch = np.ascontiguousarray(choice, np.int32)
+    adv = np.ascontiguousarray(advantage, np.float32)
+    q = None if distrib is None else np.ascontiguousarray(distrib, np.float32)
+    out = np.zeros_like(probs)
+    check(_lib.lib.xh_action_loss_grad(ctx.h, LOSSES[kind], rows, rng, _ptr(ch),
+                                       None if q is None else _ptr(q), _ptr(adv),
+                                       _ptr(probs), param, _ptr(out)))
+    return out
+
+
+def optimizer_apply(ctx, kind, params, grad, lr, weight_decay=0.0, beta1=0.9,
+                    beta2=0.999, t=1.0, m=None, v=None):
+    """optimizer::next_parameters on the device (xh_optimizer_apply); returns
+    (params, m, v), the state arrays updated in place as well."""
+    p = np.ascontiguousarray(params, np.float32).copy()
+    g = np.ascontiguousarray(grad, np.float32)
+    m = np.zeros_like(p) if m is None else m
+    v = np.zeros_like(p) if v is None else v
+    check(_lib.lib.xh_optimizer_apply(ctx.h, _lib.OPTIMIZERS[kind], lr,
+                                      weight_decay, beta1, beta2, t, _ptr(p),
+                                      _ptr(g), _ptr(m), _ptr(v), p.size))
+    return p, m, v
+
+
 def policy_param_count(dims, h1, h2):
     f0 = 2 * dims
     return h1 * f0 + h1 + h2 * h1 + h2 + h2 + 1
@@ -200,7 +318,7 @@ class Trainer:
                  lr_policy=None, lr_value=None, wd_policy=None, wd_value=None,
                  gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
                  num_envs_global=None, env_offset=0, adv_normalize=False,
-                 lr_scale_rows=False, train_grid_cap=0):
+                 lr_scale_rows=False, train_grid_cap=0, record_distrib=False):
         cfg = _lib.Config()
         a = ALGOS[algo]
         _lib.lib.xh_config_default(C.byref(cfg), a, bins, dims, num_envs, steps)
@@ -225,6 +343,7 @@ class Trainer:
         cfg.lr_scale_rows = int(bool(lr_scale_rows))
         # test-only: cap on the train workgroups (accumulation depth tests)
         cfg.train_grid_cap = int(train_grid_cap)
+        cfg.record_distrib = int(bool(record_distrib))
         self.cfg = cfg
         self.ctx = ctx
         self.B, self.D, self.N, self.T = bins, dims, num_envs, steps
@@ -274,6 +393,10 @@ class Trainer:
 
     def synchronize(self):
         self.ctx.synchronize()
+
+    def forget(self):
+        """replay_buffer::forget() without learn() (xh_trainer_forget)."""
+        check(_lib.lib.xh_trainer_forget(self.h))
 
     def set_forced_actions(self, actions):
         if actions is None:

@@ -36,6 +36,7 @@
 #include <random>
 #include <sstream>
 #include <string>
+#include <typeinfo>
 #include <vector>
 
 #include <xylo/nn.h>
@@ -179,6 +180,13 @@ class pg_learner : public xylo::policy_gradient_learner<action, observation> {
              float gamma = 0.99)
       : xylo::policy_gradient_learner<action, observation>(
             rb, action_model, action_optimizer, gamma) {}
+
+ protected:
+  // this exact class runs the fused device learner (policy_gradient.h)
+  bool device_fused() const override {
+    return typeid(*this) == typeid(pg_learner) &&
+           xylo::detail::device_fusable<action, observation>(this->desc());
+  }
 };
 
 class ac_learner : public xylo::actor_critic_learner<action, observation> {
@@ -190,6 +198,13 @@ class ac_learner : public xylo::actor_critic_learner<action, observation> {
       : xylo::actor_critic_learner<action, observation>(
             rb, action_model, action_optimizer, value_model, value_optimizer,
             gamma) {}
+
+ protected:
+  // this exact class runs the fused device learner (policy_gradient.h)
+  bool device_fused() const override {
+    return typeid(*this) == typeid(ac_learner) &&
+           xylo::detail::device_fusable<action, observation>(this->desc());
+  }
 };
 
 class ppo_learner : public xylo::ppo_learner<action, observation> {
@@ -201,6 +216,13 @@ class ppo_learner : public xylo::ppo_learner<action, observation> {
       : xylo::ppo_learner<action, observation>(rb, action_model,
                                                action_optimizer, value_model,
                                                value_optimizer, gamma) {}
+
+ protected:
+  // this exact class runs the fused device learner (policy_gradient.h)
+  bool device_fused() const override {
+    return typeid(*this) == typeid(ppo_learner) &&
+           xylo::detail::device_fusable<action, observation>(this->desc());
+  }
 };
 
 class kl_ppo_learner : public xylo::kl_ppo_learner<action, observation> {
@@ -212,6 +234,13 @@ class kl_ppo_learner : public xylo::kl_ppo_learner<action, observation> {
       : xylo::kl_ppo_learner<action, observation>(rb, action_model,
                                                   action_optimizer, value_model,
                                                   value_optimizer, gamma) {}
+
+ protected:
+  // this exact class runs the fused device learner (policy_gradient.h)
+  bool device_fused() const override {
+    return typeid(*this) == typeid(kl_ppo_learner) &&
+           xylo::detail::device_fusable<action, observation>(this->desc());
+  }
 };
 
 }  // namespace bp

@@ -100,6 +100,47 @@ inline policy_shape parse_full_policy(const xylo::model &m) {
   return s;
 }
 
+// non-throwing forms: can the device take this model?
+template <class F>
+bool parses(F &&f) {
+  try {
+    f();
+    return true;
+  } catch (const xeno::error &) {
+    return false;
+  }
+}
+inline std::pair<int, int> parse_value(const xylo::model &m);
+inline bool device_policy(const xylo::model &m) {
+  return parses([&] { parse_policy(m); });
+}
+inline bool device_full_policy(const xylo::model &m) {
+  return parses([&] { parse_full_policy(m); });
+}
+inline bool device_value(const xylo::model &m) {
+  return parses([&] { parse_value(m); });
+}
+// The fused device learner takes this description: library optimizers, the
+// per-bin policy with the learner's head (REINFORCE: the full policy) and the
+// device value net.
+inline bool fusable(const xylo::learner_desc &d) {
+  auto lib_opt = [](const xylo::optimizer *o) {
+    return !o || o->kind() != xylo::optimizer_kind::custom;
+  };
+  if (!d.action_model || !lib_opt(d.action_optimizer) ||
+      !lib_opt(d.value_optimizer))
+    return false;
+  if (d.kind == xylo::learner_kind::reinforce)
+    return device_full_policy(*d.action_model);
+  if (!d.value_model || !device_policy(*d.action_model) ||
+      !device_value(*d.value_model))
+    return false;
+  const int want = int(d.kind == xylo::learner_kind::actor_critic
+                           ? xylo::layer_kind::softmax_xent
+                           : xylo::layer_kind::softmax);
+  return parse_policy(*d.action_model).head == want;
+}
+
 inline std::pair<int, int> parse_value(const xylo::model &m) {
   using K = xylo::layer_kind;
   auto ls = m.layers();
@@ -261,8 +302,31 @@ class session {
 
   void forget() {
     flush_all();
+    if (tr_ && state_ == rolled) {
+      // the window was never learned on the device (a learner of the
+      // caller's own read it through sample_td, or nobody did): forget() is
+      // the trainer's shift of the final states to the next start states
+      check(xh_trainer_forget(tr_->h), "xh_trainer_forget");
+      state_ = idle;
+      ++steps_;
+    }
     learned_unforgotten_ = false;
   }
+
+  // learner.step() of a composed learner (policy_gradient.h) consumed the
+  // window on the host: the trainer forgets it as its own learn() would
+  void learned_on_host() {
+    flush_all();
+    if (!tr_) return;  // host-stepped experience: nothing on the device
+    if (state_ != rolled)
+      throw xeno::error("xylo-hip: learner.step() without new experience");
+    check(xh_trainer_forget(tr_->h), "xh_trainer_forget");
+    state_ = idle;
+    learned_unforgotten_ = true;
+    ++steps_;
+  }
+
+  bool composed() const { return learner_.fused && !learner_.fused(); }
 
   // replay_buffer.sample_td(): the window's trajectories from the device.
   void materialise(rb_t &rb) {
@@ -282,6 +346,13 @@ class session {
     get(XH_BUF_ITEMS, items);
     get(XH_BUF_ACTION, act);
     get(XH_BUF_DONE, done);
+    // the sampling distributions (discrete_action::distrib) when the
+    // trainer recorded them for a composed learner's loss
+    std::vector<float> qold;
+    if (tr_->cfg.record_distrib) {
+      qold.resize(std::size_t(T) * N * B);
+      get(XH_BUF_QOLD, qold);
+    }
     auto state = [&](int t, int e) {
       observation o;
       const std::int8_t *b = &bins[(std::size_t(t) * N + e) * B * 2];
@@ -298,6 +369,9 @@ class session {
         if (!traj) traj = &rb.emplace_trajectory(state(t, e));
         action a;
         a.choice = std::size_t(act[std::size_t(t) * N + e]);
+        if (!qold.empty())
+          a.distrib = xylo::vector(xylo::vector_view(
+              qold.data() + (std::size_t(t) * N + e) * B, std::size_t(B)));
         const bool over = done[std::size_t(t) * N + e] != 0;
         observation end = state(over ? t : t + 1, e);
         if (over) {  // the overflowed view before reset (rl.h:336-343)
@@ -414,7 +488,9 @@ class session {
   void push_params() {
     if (!tr_) return;
     push(*learner_.action_model, XH_POLICY, pol_version_);
-    if (learner_.value_model) push(*learner_.value_model, XH_VALUE, val_version_);
+    // a composed learner's value net never runs on this trainer
+    if (learner_.value_model && !tr_->cfg.record_distrib)
+      push(*learner_.value_model, XH_VALUE, val_version_);
   }
   bool pg() const { return tr_ && tr_->cfg.algo == XH_PG; }
 
@@ -543,19 +619,24 @@ class session {
       return;
     }
     const policy_shape ps = parse_policy(*learner_.action_model);
-    const auto vs = parse_value(*learner_.value_model);
+    // a composed learner (policy_gradient.h) learns on the host: the trainer
+    // only rolls out, recording the sampling distributions its loss reads
+    const bool composed = this->composed();
+    const auto vs = composed ? std::pair<int, int>{64, 32}
+                             : parse_value(*learner_.value_model);
     const bool ac = learner_.kind == xylo::learner_kind::actor_critic;
     const bool klppo = learner_.kind == xylo::learner_kind::kl_ppo;
     const int want_head = int(ac ? xylo::layer_kind::softmax_xent
                                  : xylo::layer_kind::softmax);
-    if (ps.head != want_head)
+    if (!composed && ps.head != want_head)
       throw xeno::error(ac ? "xylo-hip: ac_learner needs a "
                              "softmax_cross_entropy_layer head"
                            : "xylo-hip: ppo_learner / kl_ppo_learner need a "
                              "softmax_layer head");
     xh_config c;
-    xh_config_default(&c, ac ? XH_AC : klppo ? XH_KLPPO : XH_PPO,
+    xh_config_default(&c, composed ? XH_PPO : ac ? XH_AC : klppo ? XH_KLPPO : XH_PPO,
                       int(num_bins), 2, N, T_);
+    c.record_distrib = composed ? 1 : 0;
     c.policy_h1 = ps.h1;
     c.policy_h2 = ps.h2;
     c.value_h1 = vs.first;
@@ -827,10 +908,16 @@ template <> struct device_traits<bp::action, bp::observation> {
   static void learn(replay_buffer<A, S> &rb, const learner_desc &d) {
     bp::device::session_of(rb).learn(rb, d);
   }
+  static bool fusable(const learner_desc &d) { return bp::device::fusable(d); }
+  static void learned_on_host(replay_buffer<A, S> &rb) {
+    if (rb.device_state()) bp::device::session_of(rb).learned_on_host();
+  }
   static bool play_steps(agent<A, S> &a, std::size_t n) {
     auto *p = dynamic_cast<const policy_gradient_policy<A, S> *>(&a.bound_policy());
     auto *env = dynamic_cast<bp::environment *>(&a.bound_env());
-    if (!p || !env) return false;
+    // a policy network the device rollout cannot run steps on the host
+    // (react() -> model::eval, still on the device)
+    if (!p || !env || !bp::device::device_policy(p->device_model())) return false;
     bp::device::session_of(a.bound_buffer()).request_steps(*env, p->device_model(),
                                                            int(n));
     return true;
@@ -840,6 +927,7 @@ template <> struct device_traits<bp::action, bp::observation> {
     if (!env) return false;
     if (auto *sp = dynamic_cast<const policy_gradient_policy<A, S> *>(
             &a.bound_policy())) {  // REINFORCE training episodes
+      if (!bp::device::device_full_policy(sp->device_model())) return false;
       bp::device::session_of(a.bound_buffer())
           .request_train_episodes(*env, sp->device_model(), k);
       return true;

@@ -1,6 +1,7 @@
-// xylo/rl.h (xylo-hip drop-in layer): actions, trajectories, replay buffer,
-// environment / policy / agent / learner interfaces (rl.h:17-392), same names
-// and signatures.
+// xylo/rl.h (xylo-hip drop-in layer): actions (discrete_action with its loss
+// gradients, continuous_action), trajectories, replay buffer (sample_td,
+// sample_transitions, forget), environment / policy / agent / learner
+// interfaces (rl.h:17-392), same names and signatures.
 //
 // Device hook: `device_traits<A, S>` (disabled by default).  When an app
 // header specialises it (apps/bin_packing/bin_packing.h does for the
@@ -12,10 +13,16 @@
 #ifndef XYLO_HIP_COMPAT_RL_H_
 #define XYLO_HIP_COMPAT_RL_H_
 
+#include <algorithm>
+#include <cmath>
+#include <exception>
+#include <functional>
+#include <iterator>
 #include <list>
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <random>
 #include <vector>
 
 #include <xylo/nn.h>
@@ -33,8 +40,10 @@ template <typename T> vector to_vector(const T &t) {
   return result;
 }
 
-// rl.h:22-75.  The loss-gradient members (gradient_log, softmax_gradient_log,
-// clipped_gradient) are computed inside the device train kernel.
+// rl.h:22-75.  The per-action loss gradients are the reference's host
+// expressions (one row each); the batched forms the learners use
+// (policy_loss / surrogate_loss / kl_regulated_loss, policy_gradient.h) run
+// on the device.
 template <std::size_t range> struct discrete_action {
   static std::size_t cardinality() { return range; }
   std::size_t choice = 0;
@@ -45,6 +54,78 @@ template <std::size_t range> struct discrete_action {
     distrib = vector(a);
   }
   void from_vector_deterministic(vector_view a) { choice = argmax(a); }
+
+  // rl.h:33-42
+  void gradient_log(vector_view input, vector_view output,
+                    float advantage) const {
+    if (input.size() != range || output.size() != range)
+      throw std::exception();
+    output = 0;
+    float log_action_grad = 1 / input[choice];
+    float weighted_grad = log_action_grad * advantage * -1;
+    float importance_grad = input[choice] / (*distrib)[choice] * weighted_grad;
+    output[choice] = importance_grad;
+  }
+
+  // rl.h:44-52
+  void softmax_gradient_log(vector_view input, vector_view output,
+                            float advantage) const {
+    if (input.size() != range || output.size() != range)
+      throw std::exception();
+    for (std::size_t i = 0; i < range; ++i) output[i] = input[i] * advantage;
+    output[choice] -= advantage;
+  }
+
+  // rl.h:54-74 (epsilon 0.2)
+  void clipped_gradient(vector_view input, vector_view output,
+                        float advantage) const {
+    constexpr float epsilon = 0.2;
+    if (input.size() != range || output.size() != range)
+      throw std::exception();
+    output = 0;
+    float ratio = input[choice] / (*distrib)[choice];
+    float clipped_ratio = ratio;
+    if (ratio > (1 + epsilon)) {
+      clipped_ratio = 1 + epsilon;
+    } else if (ratio < (1 - epsilon)) {
+      clipped_ratio = 1 - epsilon;
+    }
+    float importance_grad =
+        std::min(clipped_ratio * advantage, ratio * advantage) * -1;
+    output[choice] = importance_grad / input[choice];
+  }
+};
+
+// rl.h:77-109: a Gaussian action with a learned mean (host arithmetic; no
+// device learner uses it).
+struct continuous_action {
+  static std::size_t cardinality() { return 1; }
+
+  float action = 0;
+  float mean = 0;
+  float stddev = 1;
+
+  void from_vector(vector_view a) {
+    vector result({1});
+    mean = a[0];
+    normal_distribution(mean, stddev, result);
+    action = result[0];
+  }
+  void gradient_log(vector_view input, vector_view output, float reward,
+                    float o_value) const {
+    if (input.size() != 1 || output.size() != 1) throw std::exception();
+    float log_action_grad = (action - input[0]) / (stddev * stddev);
+    float weighted_grad = log_action_grad * (reward / o_value - 1) * -1;
+    float normalized_input_action_diff = (action - input[0]) / stddev;
+    float normalized_action_diff = (action - mean) / stddev;
+    float importance_grad =
+        ::exp(-0.5 *
+              (normalized_input_action_diff * normalized_input_action_diff -
+               normalized_action_diff * normalized_action_diff)) *
+        weighted_grad;
+    output[0] = importance_grad;
+  }
+  void clipped_gradient(vector_view, vector_view, float, float) const {}
 };
 
 template <typename A, typename S> struct transition {
@@ -144,6 +225,38 @@ template <typename A, typename S> class replay_buffer {
       if (traj.size() == 0) continue;
       traj.fill_reference();
       result.emplace_back(traj);
+    }
+    return result;
+  }
+
+  // rl.h:236-272: n transitions drawn uniformly (with replacement) over the
+  // buffer's transitions, from a std::random_device-seeded mt19937 as the
+  // reference draws them (not reproducible run to run, as there).
+  std::vector<transition_ref<A, S>> sample_transitions(std::size_t n) {
+    if constexpr (device_traits<A, S>::enabled)
+      device_traits<A, S>::materialise(*this);
+    std::vector<transition_ref<A, S>> result;
+    result.reserve(n);
+    std::size_t total = 0;
+    for (trajectory<A, S> &traj : trajectories_) total += traj.size();
+    if (n && !total) throw xeno::error("sample_transitions: empty replay buffer");
+    std::random_device rd;
+    std::mt19937 gen(rd());
+    std::uniform_int_distribution<> distrib(0, int(total) - 1);
+    for (std::size_t i = 0; i < n; ++i) {
+      std::size_t index = std::size_t(distrib(gen)), start = 0;
+      transition<A, S> *p_trans = nullptr;
+      for (trajectory<A, S> &traj : trajectories_) {
+        const std::size_t end = start + traj.size();
+        if (index < end) {
+          auto pos = traj.transitions.begin();
+          std::advance(pos, index - start);
+          p_trans = &*pos;
+          break;
+        }
+        start = end;
+      }
+      result.emplace_back(*p_trans);
     }
     return result;
   }

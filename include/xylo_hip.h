@@ -123,6 +123,11 @@ typedef struct {
      xh_trainer_kernel_info ("train_grid", "train_grid_cap"); bench.py
      refuses a trainer with a cap. */
   int train_grid_cap;
+  /* 1: rollouts also record every step's whole sampling distribution into
+     XH_BUF_QOLD (always on for XH_KLPPO), for a learner assembled on the
+     host from the layer / loss pieces below whose loss reads it
+     (discrete_action::distrib, rl.h:27-30).  0 (default): only p_old. */
+  int record_distrib;
 } xh_config;
 
 /* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */
@@ -189,7 +194,8 @@ enum {
   XH_BUF_LOGITS = 12,  /* f32   [N][B]  logits of the last rollout step      */
   XH_BUF_PROBS = 13,   /* f32   [N][B]  probabilities of the last step       */
   XH_BUF_V_STATE0 = 14,/* f32   [T+1][N] V(S_t) before the value step        */
-  XH_BUF_QOLD = 15,    /* f32   [T][N][B] KL-PPO: sampled distributions      */
+  XH_BUF_QOLD = 15,    /* f32   [T][N][B] sampled distributions (KL-PPO, or
+                                  xh_config.record_distrib)                  */
   XH_BUF_KL = 16,      /* f32   [epochs][3] KL-PPO: beta used, mean KL, new
                                   beta of the last learn()                   */
   XH_BUF_LEN = 17,     /* int32 [N]  REINFORCE: env steps of the last rollout */
@@ -348,6 +354,76 @@ int xh_model_eval(xh_ctx *ctx, const xh_layer *layers, int nlayers,
                   const float *params, size_t nparams, const float *x,
                   int rows, int cols, float *out, size_t out_cap,
                   int *out_cols);
+
+/* ------------------------------------- layer / model / optimizer / loss -- */
+/* The reference's generic training API on the device, for callers that
+ * assemble their own learner from its pieces (the drop-in layer's
+ * xylo::layer / model / optimizer / loss functions, include/xylo_compat).
+ * Synchronous; host arrays in and out; layers and the flat parameter layout
+ * as xh_model_eval.
+ *
+ * xh_model_forward: model::forward (nn.h:481-488) -- the input and every
+ * layer's output, each rows x widths[l], concatenated into acts (widths[0] =
+ * cols, widths[nlayers] = the output's).  acts_cap floats; widths has
+ * nlayers + 1 entries. */
+int xh_model_forward(xh_ctx *ctx, const xh_layer *layers, int nlayers,
+                     const float *params, size_t nparams, const float *x,
+                     int rows, int cols, float *acts, size_t acts_cap,
+                     int *widths);
+/* model::gradient (nn.h:510-528): `inputs` = the first nlayers matrices of
+ * model::forward, concatenated as xh_model_forward writes them; target =
+ * dL/d(output), rows x target_cols.  Backpropagates from the last layer
+ * (layer::gradient then layer::backward per layer, layer 0 gradient only)
+ * into grad[nparams] (model::parameters() layout). */
+int xh_model_gradient(xh_ctx *ctx, const xh_layer *layers, int nlayers,
+                      const float *params, size_t nparams, const float *inputs,
+                      int rows, int cols, const float *target, int target_cols,
+                      float *grad);
+/* layer::backward / layer::gradient (nn.h:20-33) of one layer: input rows x
+ * cols, backprop rows x bp_cols (the layer's output width).  backward ->
+ * out rows x cols (full / conv1d_1: backprop . A; relu: gated by input > 0;
+ * softmax: the Jacobian product; softmax_cross_entropy: backprop itself);
+ * gradient -> grad[ngrad], the layer's [dA (out x in), db (out)] (ngrad = 0
+ * for activations). */
+int xh_layer_backward(xh_ctx *ctx, const xh_layer *layer, const float *params,
+                      size_t nparams, const float *input, int rows, int cols,
+                      const float *backprop, int bp_cols, float *out);
+int xh_layer_gradient(xh_ctx *ctx, const xh_layer *layer, const float *input,
+                      int rows, int cols, const float *backprop, int bp_cols,
+                      float *grad, size_t ngrad);
+/* The discrete-action loss gradients of a batch of `rows` actions over
+ * `range` choices, out[rows][range] (rl.h:33-74 per row):
+ *   XH_LOSS_GRADIENT_LOG          discrete_action::gradient_log
+ *   XH_LOSS_SOFTMAX_GRADIENT_LOG  softmax_gradient_log = policy_loss
+ *                                 (policy_gradient.h:24-34)
+ *   XH_LOSS_CLIPPED               clipped_gradient = surrogate_loss
+ *                                 (:36-46), param = epsilon (0.2)
+ *   XH_LOSS_KL_REGULATED          the gradient of kl_regulated_loss (:55-74):
+ *                                 softmax_gradient_log + param (beta) times
+ *                                 (probs - distrib); the beta adaptation is
+ *                                 the caller's
+ * choice[rows], advantage[rows], probs = the model's output rows (the
+ * reference's orig_action_matrix), distrib = each action's sampling
+ * distribution [rows][range] (unused by SOFTMAX_GRADIENT_LOG, may be NULL
+ * there). */
+enum { XH_LOSS_GRADIENT_LOG = 0, XH_LOSS_SOFTMAX_GRADIENT_LOG = 1,
+       XH_LOSS_CLIPPED = 2, XH_LOSS_KL_REGULATED = 3 };
+int xh_action_loss_grad(xh_ctx *ctx, int kind, int rows, int range,
+                        const int32_t *choice, const float *distrib,
+                        const float *advantage, const float *probs, float param,
+                        float *out);
+/* optimizer::next_parameters (nn.h:616-698) of n parameters in place:
+ * XH_OPT_SGD p (1 - wd) - g lr; XH_OPT_MOMENTUM v = 0.9 v + g, p - v lr (m =
+ * v); XH_OPT_ADAM moments m, v, bias-corrected with step t (1, 2, ...),
+ * p - m^ lr / (sqrt(v^) + 1e-7).  m / v: the caller's state arrays (NULL for
+ * sgd). */
+int xh_optimizer_apply(xh_ctx *ctx, int kind, float lr, float weight_decay,
+                       float beta1, float beta2, float t, float *params,
+                       const float *grad, float *m, float *v, size_t n);
+/* replay_buffer::forget() (rl.h:274-291) after a learn() that did not run on
+ * this trainer (a learner assembled from the pieces above consumed the
+ * batch): the batch's final states become the next rollout's start states. */
+int xh_trainer_forget(xh_trainer *t);
 
 /* sizeof of the ABI structs ("xh_config", "xh_eval", "xh_layer"; 0 if
  * unknown), so a

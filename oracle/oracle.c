@@ -1239,6 +1239,25 @@ void or_value_grad_rows(const or_model *m, const float *params, const float *x,
   or_model_grad(m, params, x, rows, xcols, loss_square, &sc, grad);
 }
 
+void or_policy_grad_rows_mag(const or_model *m, const float *params,
+                             const float *x, int rows, int xcols,
+                             const int32_t *choice, const float *pold,
+                             const float *adv, int algo, float *grad,
+                             float *mag) {
+  int *ch = (int *)malloc(sizeof(int) * (rows > 0 ? rows : 1));
+  for (int r = 0; r < rows; ++r) ch[r] = choice[r];
+  pl_ctx pc = {ch, pold, adv, algo == OR_PPO, NULL, NULL, 0, 0};
+  or_model_grad_mag(m, params, x, rows, xcols, loss_policy, &pc, grad, mag);
+  free(ch);
+}
+
+void or_value_grad_rows_mag(const or_model *m, const float *params,
+                            const float *x, int rows, int xcols,
+                            const float *targets, float *grad, float *mag) {
+  sq_ctx sc = {targets};
+  or_model_grad_mag(m, params, x, rows, xcols, loss_square, &sc, grad, mag);
+}
+
 /* deep_agent.cc:25-41 / policy_gradient_deterministic_policy
  * (policy_gradient.h:356-373): argmax over the model output. */
 double or_eval_argmax(const or_env_cfg *c, const or_model *pol,

@@ -173,6 +173,16 @@ void or_policy_grad_rows(const or_model *m, const float *params, const float *x,
                          float *grad);
 void or_value_grad_rows(const or_model *m, const float *params, const float *x,
                         int rows, int xcols, const float *targets, float *grad);
+/* The same two with, per gradient entry, the sum of |terms| of its row sums
+ * (the rounding scale of or_model_grad_mag). */
+void or_policy_grad_rows_mag(const or_model *m, const float *params,
+                             const float *x, int rows, int xcols,
+                             const int32_t *choice, const float *pold,
+                             const float *adv, int algo, float *grad,
+                             float *mag);
+void or_value_grad_rows_mag(const or_model *m, const float *params,
+                            const float *x, int rows, int xcols,
+                            const float *targets, float *grad, float *mag);
 
 /* Deterministic (argmax) evaluation, deep_agent.cc:25-41: `episodes` episodes
  * on one env seeded at x0; returns total reward, engine state via *x. */

@@ -86,6 +86,13 @@ def lib():
                                           C.c_void_p, C.c_int, C.c_void_p]
         l.or_value_grad_rows.argtypes = [C.POINTER(Model), C.c_void_p, C.c_void_p,
                                          C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        l.or_policy_grad_rows_mag.argtypes = [C.POINTER(Model), C.c_void_p,
+                                              C.c_void_p, C.c_int, C.c_int,
+                                              C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_int, C.c_void_p, C.c_void_p]
+        l.or_value_grad_rows_mag.argtypes = [C.POINTER(Model), C.c_void_p,
+                                             C.c_void_p, C.c_int, C.c_int,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
         l.or_eval_argmax.restype = C.c_double
         l.or_eval_argmax.argtypes = [C.POINTER(EnvCfg), C.POINTER(Model),
                                      C.c_void_p, C.c_long, u32p]
@@ -359,6 +366,34 @@ def value_grad_rows(model, params, x, targets):
     lib().or_value_grad_rows(C.byref(model), _ptr(params), _ptr(x), x.shape[0],
                              x.shape[1], _ptr(tg), _ptr(g))
     return g
+
+
+def policy_grad_rows_mag(model, params, x, choice, pold, adv, algo):
+    """(gradient, per-entry sum of |terms|) of the policy loss over rows."""
+    x = np.ascontiguousarray(x, np.float32)
+    params = np.ascontiguousarray(params, np.float32)
+    ch = np.ascontiguousarray(choice, np.int32)
+    pold = np.ascontiguousarray(pold, np.float32)
+    adv = np.ascontiguousarray(adv, np.float32)
+    g = np.zeros(nparams(model), np.float32)
+    mag = np.zeros(nparams(model), np.float32)
+    lib().or_policy_grad_rows_mag(C.byref(model), _ptr(params), _ptr(x),
+                                  x.shape[0], x.shape[1], _ptr(ch), _ptr(pold),
+                                  _ptr(adv), algo, _ptr(g), _ptr(mag))
+    return g, mag
+
+
+def value_grad_rows_mag(model, params, x, targets):
+    """(gradient, per-entry sum of |terms|) of the square loss over rows."""
+    x = np.ascontiguousarray(x, np.float32)
+    params = np.ascontiguousarray(params, np.float32)
+    tg = np.ascontiguousarray(targets, np.float32)
+    g = np.zeros(nparams(model), np.float32)
+    mag = np.zeros(nparams(model), np.float32)
+    lib().or_value_grad_rows_mag(C.byref(model), _ptr(params), _ptr(x),
+                                 x.shape[0], x.shape[1], _ptr(tg), _ptr(g),
+                                 _ptr(mag))
+    return g, mag
 
 
 OR_HEUR = {"random": 0, "firstfit": 1, "bestfit": 2, "minwaste": 3}
