@@ -20,8 +20,9 @@ pytestmark = pytest.mark.gpu
 
 # (relative L2, worst entry / max |g|) between the shard sum and the full
 # batch at B = 64, n = 16384 (no oracle at that size): about 3x the measured
-# values (r03: 2.9e-4 relative L2; profiles/r04*_shard_sums.jsonl)
-SHARD_SUM_LIMITS_B64 = (1e-3, 4e-3)
+# values (r03: 2.9e-4 relative L2; r04: 4.9e-4 / 1.4e-3,
+# profiles/r04*_shard_sums.jsonl)
+SHARD_SUM_LIMITS_B64 = (1.5e-3, 4e-3)
 
 
 def _log_shard_sum(B, n, it, rel, worst):
@@ -32,8 +33,8 @@ def _log_shard_sum(B, n, it, rel, worst):
     d = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(d):
         with open(os.path.join(d, "shard_sums.jsonl"), "a") as f:
-            f.write(json.dumps({"B": B, "n": n, "it": it, "rel_l2": rel,
-                                "worst_rel": worst}) + "\n")
+            f.write(json.dumps({"B": B, "n": n, "it": it, "rel_l2": float(rel),
+                                "worst_rel": float(worst)}) + "\n")
 
 
 @pytest.mark.parametrize("B,D,widths,n", [
@@ -116,8 +117,8 @@ def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
             # same kernels is the n = 128 case).  Policy-gradient entries
             # cancel to ~1e-3 of their sum |terms| (conftest), so at 8.4 M
             # rows two summation orders differ by ~1e-4 of |g|.  Limits =
-            # about 3x the measured values (r03: 2.9e-4 relative L2 at 64
-            # bins, 2e-6 at 8 bins; the measured pair is logged per run)
+            # about 3x the measured values (SHARD_SUM_LIMITS_B64; 2e-6 at 8
+            # bins; the measured pair is logged per run)
             rel = np.linalg.norm(g - f) / np.linalg.norm(f)
             worst = np.abs(g - f).max() / np.abs(f).max()
             lim = (1e-5, 1e-4) if B == 8 else SHARD_SUM_LIMITS_B64
