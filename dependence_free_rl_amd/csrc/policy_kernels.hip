@@ -325,23 +325,27 @@ __device__ __forceinline__ float logit_part(const float *lds, const f32x16 &pre,
 
 // Softmax of the candidate-bin scores z (lane = row = bin of env `env`,
 // whose B rows sit in lanes seg0 ..), the categorical sample (or the forced
-// action), and the env transition into slot t+1 (rl.h:325-349,
+// action), and the env transition of slot t into slot t+1 (rl.h:325-349,
 // bin_packing.h:53-79).  `cur` holds this lane's raw row (rows lr / 32+lr).
+// x is the env's minstd state (the same in every lane of the segment; the
+// caller loads and stores it), `last` marks the launch's last step (the
+// optional logits / probabilities outputs).  Out: nbv = this lane's bin in
+// slot t+1, first = the env's next item is item_a.
 template <class S>
-__device__ __forceinline__ void sample_step(const RolloutArgs &a, float z,
-                                            int env, int seg0, int bin,
-                                            const RowRaw<S> &cur) {
+__device__ __forceinline__ void sample_step_x(const RolloutArgs &a, int t, bool last,
+                                              float z, int env, int seg0, int bin,
+                                              const RowRaw<S> &cur, uint32_t &x,
+                                              int (&nbv)[S::D], bool &first) {
   constexpr int B = S::B;
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int N = a.b.N, t = a.t;
+  const int N = a.b.N;
   const float ex = expf(z);
   const float sum = seg_sum<B>(ex);
   const float p = ex / sum;
-  if (a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
-  if (a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
+  if (last && a.logits_out) a.logits_out[(size_t)env * B + bin] = z;
+  if (last && a.probs_out) a.probs_out[(size_t)env * B + bin] = p;
   if (a.qold_out) a.qold_out[((size_t)t * N + env) * B + bin] = p;
 
-  uint32_t x = a.b.rng[env];
   int choice;
   if (a.forced) {
     choice = a.forced[(size_t)t * N + env];
@@ -363,10 +367,13 @@ __device__ __forceinline__ void sample_step(const RolloutArgs &a, float z,
   }
   const int done = __shfl(neg, seg0 + choice, kWave);
   // apply -> get_item, or game over -> reset -> get_item: 2 draws either way
-  const bool first = canonical(x) < a.env.p_a;
+  first = canonical(x) < a.env.p_a;
   int8_t *ob = a.b.bins + ((size_t)(t + 1) * N + env) * S::BD + bin * S::D;
 #pragma unroll
-  for (int d = 0; d < S::D; ++d) ob[d] = (int8_t)(done ? kCapacity : nb[d]);
+  for (int d = 0; d < S::D; ++d) {
+    nbv[d] = done ? kCapacity : nb[d];
+    ob[d] = (int8_t)nbv[d];
+  }
   if (bin == 0) {
     int8_t *oi = a.b.items + ((size_t)(t + 1) * N + env) * 4;
 #pragma unroll
@@ -375,8 +382,20 @@ __device__ __forceinline__ void sample_step(const RolloutArgs &a, float z,
     a.b.action[(size_t)t * N + env] = choice;
     a.b.pold[(size_t)t * N + env] = pold;
     a.b.done[(size_t)t * N + env] = (uint8_t)done;
-    a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
   }
+}
+
+// One step (slot a.t) of env `env`: sample_step_x with the stream state read
+// from and written back to a.b.rng (jumped after step T-1).
+template <class S>
+__device__ __forceinline__ void sample_step(const RolloutArgs &a, float z,
+                                            int env, int seg0, int bin,
+                                            const RowRaw<S> &cur) {
+  uint32_t x = a.b.rng[env];
+  int nbv[S::D];
+  bool first;
+  sample_step_x<S>(a, a.t, true, z, env, seg0, bin, cur, x, nbv, first);
+  if (bin == 0) a.b.rng[env] = (a.t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
 }
 
 // =========================================================== rollout step ==
@@ -621,7 +640,7 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
 }
 
 // ============================== rollout step, wave per env, f16 pairs ==
-// The wave-per-env rollout of the [128,128] shapes with layer 2 on the f16
+// The wave-per-group rollout of the [128,128] and [64,64] shapes with layer 2 on the f16
 // matrix cores at f32-class accuracy (xh_split.h, f16 pairs: W2 and H1 each
 // scaled by a power of two chosen per launch -- max|W2|, and the bound
 // |H1[r][i]| <= sum_k |W1[i][k]| + |b1[i]| since every observation feature
@@ -640,12 +659,13 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
 // biases enter as the MFMA chains' C inputs.  The logits differ from rollout_wave_kernel's in the
 // last places (f32-class: tests/test_gpu_scale.py); the sampler, the env
 // step and everything after are the same code.
-// LDS (bytes): two W2 part images [o][permuted i] (64 KB), then f32 W1
-// [H1][F0], b1, b2 S_W S_H, w3 / (S_W S_H), b3, S_H, the scale reduction.
+// LDS (bytes): two W2 part images [o][permuted i] (H2 rows of 256 bytes: 64
+// KB at [128,128]), then f32 W1 [H1][F0], b1, b2 S_W S_H, w3 / (S_W S_H), b3,
+// S_H, the scale reduction.
 template <class S>
 struct RollSplitLds {
   static constexpr int W2 = 0;
-  static constexpr int F = 2 * 128 * kImgRow;
+  static constexpr int F = 2 * S::H2 * kImgRow;
   static constexpr int W1 = 0, B1 = S::H1 * S::F0, B2 = B1 + S::H1, W3 = B2 + S::H2,
                        B3 = W3 + S::H2, SH = B3 + 1, SC = B3 + 4;
   static constexpr size_t bytes = F + sizeof(float) * (SC + 2 * 16);
@@ -687,14 +707,14 @@ __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
   }
   const float SW = f16_scale_for(MW), SH = f16_scale_for(MH), S2 = SW * SH;
   for (int e = threadIdx.x; e < S::H2 * S::H1; e += blockDim.x) {
-    const int o = e >> 7, i = e & 127;
+    const int o = e / S::H1, i = e % S::H1;
     // logical column i -> its slot: bits 2 and 3 swapped within the 16-block
     const int c = (i & ~12) | ((i & 4) << 1) | ((i & 8) >> 1);
     _Float16 x0, x1;
     split2h(P[PL.oW2() + e] * SW, x0, x1);
     const int off = img_off(o, c >> 3) + 2 * (c & 7);
     *reinterpret_cast<_Float16 *>(lds + L::W2 + off) = x0;
-    *reinterpret_cast<_Float16 *>(lds + L::W2 + 128 * kImgRow + off) = x1;
+    *reinterpret_cast<_Float16 *>(lds + L::W2 + S::H2 * kImgRow + off) = x1;
   }
   // layer 1 staged times S_H (its output is H1 S_H exactly: a power of two),
   // b2 times S_W S_H (layer 2's C input), w3 divided by it
@@ -720,7 +740,7 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
   using L = RollSplitLds<S>;
   const float *lf = reinterpret_cast<const float *>(lds + L::F);
   const int lane = threadIdx.x & 63, lr = lane & 31, h = lane >> 5;
-  const char *w2i[2] = {lds + L::W2, lds + L::W2 + 128 * kImgRow};
+  const char *w2i[2] = {lds + L::W2, lds + L::W2 + S::H2 * kImgRow};
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     float xb[S::S1];
@@ -728,9 +748,9 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
     for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
     // layer 2's accumulators start at b2 S_W S_H (C layout: register 4q + u
     // = feature ot*32 + 8q + 4h + u)
-    f32x16s pre[4];
+    f32x16s pre[S::NOT];
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
+    for (int ot = 0; ot < S::NOT; ++ot)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B2 + ot * 32 + 8 * q + 4 * h);
@@ -742,7 +762,7 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
     // (fully unrolled: the next tile's layer 1 and split schedule beside this
     // tile's layer-2 MFMAs; 0.75 -> 0.72 ms per config-3 iteration)
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < S::NIT; ++it) {
       // layer-1 tile it, times S_H: the bias as the chain's C input, relu
       f32x16 t1;
 #pragma unroll
@@ -768,7 +788,7 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
         bfr[j >> 3][1][j & 7] = p1;
       }
 #pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
+      for (int ot = 0; ot < S::NOT; ++ot) {
         const int rb = row_base(ot * 32 + lr, h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -786,7 +806,7 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
     }
     float z = 0.0f;
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
+    for (int ot = 0; ot < S::NOT; ++ot) {
       float zp = 0.0f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -801,24 +821,64 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
   }
 }
 
+// The split rollout over whole row groups of 64 (one env of 64 bins, or two
+// of 32: G = 64 / B envs, env e0 + h in lane half h), WAVES waves per
+// workgroup, each wave stepping its group through slots a.t .. a.t +
+// a.nsteps - 1 in one launch: slot t+1's rows come from the sampler's
+// registers (this lane's row, the partner half's by a lane swap), the minstd
+// state stays in a register and is stored once, after the launch's last
+// step.  Per step the same operations as one launch per step, so states,
+// actions and logits are bit-identical to stepping slot by slot.
 template <class S>
-__global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rollout_split_kernel(RolloutArgs a) {
-  static_assert(S::B == 64 && S::NIT == 4 && S::NOT == 4,
-                "split rollout: B=64, [128,128]");
+constexpr int roll_split_waves() { return S::B == 64 ? kRollWaves64 : 4; }
+template <class S>
+constexpr int roll_split_occ() { return S::B == 64 ? roll_occ(kRollWaves64) : 2; }
+
+template <class S>
+__global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) void rollout_split_kernel(RolloutArgs a) {
+  static_assert((S::B == 64 && S::NIT == 4 && S::NOT == 4) ||
+                    (S::B == 32 && S::NIT == 2 && S::NOT == 2),
+                "split rollout: B=64 [128,128] or B=32 [64,64]");
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   char *lds = reinterpret_cast<char *>(ldsf);
   stage_split_rollout<S>(a.params, lds);
   __syncthreads();
   const float b3 = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F)[RollSplitLds<S>::B3];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int wpb = blockDim.x >> 6;
-  for (int env = blockIdx.x * wpb + w; env < a.b.N; env += gridDim.x * wpb) {
+  const int ngroups = a.b.N / S::G;
+  const int t_last = a.t + (a.nsteps > 1 ? a.nsteps : 1) - 1;
+  // lane = row 32 h + lr of the group: env e0 + h and bin lr when G = 2,
+  // bin = lane when G = 1
+  const int eoff = S::G == 2 ? h : 0, seg0 = S::G == 2 ? 32 * h : 0;
+  const int bin = S::G == 2 ? lr : lane;
+  for (int g = blockIdx.x * wpb + w; g < ngroups; g += gridDim.x * wpb) {
+    const int e0 = g * S::G, env = e0 + eoff;
     RowRaw<S> cur;
-    fetch_rows<S>(a.b, a.t, env, cur);
-    float zl[2];
-    wave_logits_split<S>(lds, cur, zl);
-    const float z = (h ? zl[1] : zl[0]) + b3;
-    sample_step<S>(a, z, env, 0, lane, cur);
+    fetch_rows<S>(a.b, a.t, e0, cur);
+    uint32_t x = a.b.rng[env];
+    for (int t = a.t; t <= t_last; ++t) {
+      float zl[2];
+      wave_logits_split<S>(lds, cur, zl);
+      const float z = (h ? zl[1] : zl[0]) + b3;
+      int nbv[S::D];
+      bool first;
+      sample_step_x<S>(a, t, t == t_last, z, env, seg0, bin, cur, x, nbv, first);
+      if (t < t_last) {
+        // rows lr / 32 + lr of slot t+1: this half's and the partner's
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) {
+          const int own = nbv[d], oth = __shfl_xor(own, 32, kWave);
+          const int ito = first ? a.env.item_a[d] : a.env.item_b[d];
+          const int itp = S::G == 2 ? __shfl_xor(ito, 32, kWave) : ito;
+          cur.bv[0][d] = h ? oth : own;
+          cur.bv[1][d] = h ? own : oth;
+          cur.iv[0][d] = h ? itp : ito;
+          cur.iv[1][d] = h ? ito : itp;
+        }
+      }
+    }
+    if (bin == 0) a.b.rng[env] = (t_last == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
   }
 }
 
@@ -2331,11 +2391,13 @@ int policy_train_grid(int B, int D, int H1, int H2, int kl) {
   return cu_count();
 }
 
-hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
-                               hipStream_t s, KernelInfo *info) {
+// One launch: slot a.t (multi = false), or slots a.t .. a.t + a.nsteps - 1
+// by the register-stepping split kernel (multi = true).
+static hipError_t launch_rollout_one(const RolloutArgs &a, int H1, int H2,
+                                     int grid, hipStream_t s, KernelInfo *info,
+                                     bool &multi) {
   const int B = a.env.B, D = a.env.D;
-  KernelInfo dummy;
-  if (!info) info = &dummy;
+  multi = false;
   info->math = kMathF32Mfma;
 #define X(XB, XD, XH1, XH2)                                                  \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {                        \
@@ -2392,7 +2454,8 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
         return hipGetLastError();                                            \
       }                                                                      \
     }                                                                        \
-    if constexpr (S::B == 64 && S::NIT == 4 && S::NOT == 4) {                \
+    if constexpr ((S::B == 64 && S::NIT == 4 && S::NOT == 4) ||             \
+                  (S::B == 32 && S::NIT == 2 && S::NOT == 2)) {              \
       if (rollout_split() && !a.wide) {                                      \
         static bool sattr = false;                                           \
         if (!sattr) {                                                        \
@@ -2401,11 +2464,14 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
                                     (int)RollSplitLds<S>::bytes);               \
           sattr = true;                                                      \
         }                                                                    \
-        constexpr int kRW = kRollWaves64;                                    \
+        constexpr int kRW = roll_split_waves<S>();                           \
         const int wg = (ng + kRW - 1) / kRW;                                 \
-        const int wgr = kRW == 8 ? grid : cu_count();                        \
+        /* 64 bins: one 12-wave workgroup per CU; 32 bins: every group's  */ \
+        /* wave resident at once (2048 groups at config 2)                */ \
+        const int wgr = S::B == 64 ? (kRW == 8 ? grid : cu_count()) : wg;    \
         info->name = "rollout_split_kernel";                                 \
         info->math = kMathSplitRollout;                                      \
+        multi = true;                                                        \
         hipLaunchKernelGGL(rollout_split_kernel<S>,                          \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            RollSplitLds<S>::bytes, s, a);                       \
@@ -2444,6 +2510,25 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
   XH_POLICY_SHAPES(X)
 #undef X
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
+                               hipStream_t s, KernelInfo *info) {
+  KernelInfo dummy;
+  if (!info) info = &dummy;
+  const int n = a.nsteps > 1 ? a.nsteps : 1;
+  bool multi = false;
+  hipError_t e = launch_rollout_one(a, H1, H2, grid, s, info, multi);
+  // a one-slot kernel ran slot a.t (its logits / probabilities are rewritten
+  // by the later slots'); the rest in one launch if the kernel allows
+  for (int k = 1; e == hipSuccess && !multi && k < n; ++k) {
+    RolloutArgs ak = a;
+    ak.t = a.t + k;
+    ak.nsteps = n - k;
+    ak.wide = 0;  // `wide` describes slot a.t only
+    e = launch_rollout_one(ak, H1, H2, grid, s, info, multi);
+  }
+  return e;
 }
 
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,

@@ -70,6 +70,10 @@ struct RolloutArgs {
   float *qold_out;        // KL-PPO: [T][N][B] the sampled distribution
   int wide;  // slot t holds a bin below -capacity: the f32-MFMA kernels run
              // (the f16-pair ones bound |bins / capacity| by 1)
+  int nsteps;  // slots t .. t + nsteps - 1 (0 = 1); logits_out / probs_out
+               // receive the last one's.  launch_rollout_step runs them in
+               // one launch where the kernel steps in registers
+               // (rollout_split_kernel), else one launch per slot
 };
 
 struct PolicyTrainArgs {

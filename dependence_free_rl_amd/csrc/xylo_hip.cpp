@@ -588,16 +588,18 @@ int do_rollout(xh_trainer *t) {
   a.params = t->pp;
   a.forced = t->use_forced ? t->forced : nullptr;
   a.qold_out = t->qold;  // KL-PPO only (nullptr otherwise)
-  for (int step = 0; step < (int)T; ++step) {
-    a.t = step;
-    a.wide = t->bins_wide[step];
-    const bool last = step == (int)T - 1;
-    a.logits_out = last ? t->logits : nullptr;
-    a.probs_out = last ? t->probs : nullptr;
-    CHK(timed(t, "rollout_step", [&]() {
-      return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
-                                     t->rgrid, s, &t->last_rollout);
-    }));
+  // all T slots in one call (one launch where the kernel steps in registers);
+  // only slot 0 can hold a wide state
+  a.t = 0;
+  a.nsteps = (int)T;
+  a.wide = t->bins_wide[0];
+  a.logits_out = t->logits;
+  a.probs_out = t->probs;
+  CHK(timed(t, "rollout_step", [&]() {
+    return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
+                                   t->rgrid, s, &t->last_rollout);
+  }));
+  for (size_t step = 0; step < T; ++step) {
     t->items_ok[step + 1] = 1;  // items drawn from the table (get_item)
     t->bins_wide[step + 1] = 0;  // apply + reset on game over: bins >= 0
   }

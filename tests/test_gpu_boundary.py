@@ -128,6 +128,47 @@ def test_overflowed_start_states_run_the_f32_kernels(ctx, monkeypatch, B, D,
     assert np.isfinite(wide["params"]).all()
 
 
+@pytest.mark.parametrize("B,D,widths", [(64, 2, (128, 128)), (32, 1, (64, 64))])
+def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths):
+    """T = 4 with an overflowed slot 0: slot 0 runs on the f32 rollout, slots
+    1-3 in one launch of the register-stepping split kernel.  Teacher-forced
+    with the all-f32 run's actions, every state, item, done and RNG state is
+    bit-identical to that run, and p_old agrees to f32 rounding."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
+                                                BUF_ITEMS, BUF_POLD, BUF_RNG)
+    N, T = 64, 4
+    pp, vp = init_policy(D, *widths, seed=15), init_value(B, D, seed=16)
+
+    def run(f32, forced=None):
+        if f32:
+            monkeypatch.setenv("XH_ROLLOUT_KERNEL", "f32")
+        else:
+            monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
+        tr = Trainer(ctx, algo="ppo", bins=B, dims=D, num_envs=N, steps=T,
+                     widths=widths, rng_state=91)
+        tr.set_params(POLICY, pp)
+        tr.set_params(VALUE, vp)
+        bins, items = tr.env_state()
+        bins[5, 3, 0] = -40
+        tr.set_env_state(0, bins, items)
+        if forced is not None:
+            tr.set_forced_actions(forced)
+        tr.rollout()
+        out = {b: tr.buffer(b).copy()
+               for b in (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_POLD, BUF_RNG)}
+        out["kinfo"] = tr.kernel_info()
+        tr.close()
+        return out
+
+    ref = run(True)
+    got = run(False, forced=ref[BUF_ACTION])
+    assert got["kinfo"]["rollout_step"]["kernel"] == "rollout_split_kernel"
+    for b in (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_RNG):
+        np.testing.assert_array_equal(got[b], ref[b], err_msg="buffer %d" % b)
+    np.testing.assert_allclose(got[BUF_POLD], ref[BUF_POLD], rtol=2e-5, atol=1e-7)
+
+
 def test_env_overrides_of_many_envs(ctx):
     """xh_trainer_set_env_state for every env (one run of consecutive envs)
     and for scattered envs: the next rollout starts from exactly those
@@ -155,8 +196,9 @@ def test_env_overrides_of_many_envs(ctx):
 @pytest.mark.parametrize("B,D,widths,train,roll,prod,f32_train", [
     (64, 2, (128, 128), HEADLINE_TRAIN_KERNEL, "rollout_split_kernel", 8.0 / 3.0,
      "policy_train8_kernel"),
-    # config 2's shape: the split train kernel, the f32 rollout
-    (32, 1, (64, 64), "policy_train_split4h_kernel", "rollout_step_kernel", 8.0 / 3.0,
+    # config 2's shape: the split train kernel and the split rollout (two
+    # envs per wave)
+    (32, 1, (64, 64), "policy_train_split4h_kernel", "rollout_split_kernel", 8.0 / 3.0,
      "policy_train_kernel"),
     (8, 2, (128, 64), None, None, None, None),
 ])

@@ -385,11 +385,13 @@ def test_split_train_kernel_accuracy(ctx, monkeypatch, algo, B, D, N, T, widths)
 
 
 @pytest.mark.parametrize("algo,N,B,D,T", [("ppo", 32768, 64, 2, 4),
-                                         ("ac", 16384, 128, 3, 8)])
+                                         ("ac", 16384, 128, 3, 8),
+                                         ("ppo", 4096, 32, 1, 4)])
 def test_split_rollout_matches_f32(ctx, monkeypatch, algo, N, B, D, T):
-    """Config-3 / config-5 size: the default 64- and 128-bin rollouts run
-    layer 2 on the bf16 matrix cores with exactly split f32 operands
-    (rollout_split_kernel / rollout_split128_kernel).
+    """Config-3 / config-5 / config-2 size: the default 64-, 128- and 32-bin
+    rollouts run layer 2 on the f16 matrix cores with exactly split f32
+    operands (rollout_split_kernel, all T slots in one launch, /
+    rollout_split128_kernel).
     Teacher-forced with the f32 wave kernel's actions, it reproduces the
     states, items, dones and RNG streams bit for bit and the logits /
     probabilities / p_old within f32-class rounding; free-running, it picks
@@ -398,7 +400,8 @@ def test_split_rollout_matches_f32(ctx, monkeypatch, algo, N, B, D, T):
     from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
                                                 BUF_ITEMS, BUF_LOGITS, BUF_POLD,
                                                 BUF_PROBS, BUF_RNG)
-    pp, vp = init_policy(D, 128, 128, seed=21), init_value(B, D, seed=22)
+    H = (64, 64) if B == 32 else (128, 128)
+    pp, vp = init_policy(D, *H, seed=21), init_value(B, D, seed=22)
     bufs = (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_LOGITS, BUF_POLD,
             BUF_PROBS, BUF_RNG)
 
@@ -408,7 +411,7 @@ def test_split_rollout_matches_f32(ctx, monkeypatch, algo, N, B, D, T):
         else:
             monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
-                     widths=(128, 128), rng_state=77)
+                     widths=H, rng_state=77)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         if forced is not None:
