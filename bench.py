@@ -64,8 +64,9 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 # split rollouts' layer 2 on f16 pairs: dense 2500 / 3.
 # Diagnostic variables that steer kernel selection (the bench refuses them
 # unless --allow-kernel-override is given):
-KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL")
+KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL", "XH_VALUE_KERNEL")
 HBM_PEAK_GBS = 8000.0
+PHASE_ITERS = 2  # the phase-breakdown pass after the timed region
 
 
 def kernel_roofline(k, flops_per_launch, avg_ms):
@@ -218,7 +219,7 @@ def main():
                          "config's; SURVEY 8(d)'s larger-T throughput point)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--allow-kernel-override", action="store_true",
-                    help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL are "
+                    help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL / XH_VALUE_KERNEL are "
                          "set (A/B measurements; the line records them)")
     ap.add_argument("--reference-lr", action="store_true",
                     help="raw lr on row sums as the reference (diverges at "
@@ -277,7 +278,11 @@ def main():
     tr.synchronize()
     if rdzv:
         rdzv.barrier()
-    tr.set_timing(True)
+    # inside the timed region only the policy train launches carry HIP events
+    # (the dominant kernel's average duration); per-launch events on every
+    # launch cost ~2 us each (config 2: 0.40 -> 0.47 ms per iteration), so the
+    # phase breakdown comes from a separate pass after the timed region
+    tr.set_timing("train")
     tr.reset_timing()
     t0 = time.perf_counter()
     tr.iterate(args.steps)
@@ -292,10 +297,16 @@ def main():
     # parameters / probabilities, done rate and mean episode length
     health = tr.health()
     ms_pt, n_pt = tr.kernel_time("policy_train")
-    ms_ro, n_ro = tr.kernel_time("rollout_step")
-    ms_v, _ = tr.kernel_time("value")
-    ms_r, _ = tr.kernel_time("reduce_sgd")
-    ms_a, _ = tr.kernel_time("allreduce")
+    # the phase breakdown: PHASE_ITERS more iterations (every rank), every
+    # launch timed
+    tr.set_timing(True)
+    tr.reset_timing()
+    tr.iterate(PHASE_ITERS)
+    tr.synchronize()
+    ph = {k: tr.kernel_time(k)[0] / PHASE_ITERS
+          for k in ("rollout_step", "policy_train", "value", "reduce_sgd",
+                    "allreduce")}
+    tr.set_timing(False)
     env_steps = n * world * T * args.steps
     value = env_steps / dt
     # dominant kernel: policy_train (one PPO epoch over N*T env-steps);
@@ -391,11 +402,13 @@ def main():
         "kernels": kinfo,
         "runtime": runtime_info(),
         "phase_ms_per_step": {
-            "rollout": round(ms_ro / args.steps, 3),
-            "policy_train": round(ms_pt / args.steps, 3),
-            "value": round(ms_v / args.steps, 3),
-            "reduce_sgd": round(ms_r / args.steps, 3),
-            "allreduce": round(ms_a / args.steps, 3)},
+            "rollout": round(ph["rollout_step"], 3),
+            "policy_train": round(ph["policy_train"], 3),
+            "value": round(ph["value"], 3),
+            "reduce_sgd": round(ph["reduce_sgd"], 3),
+            "allreduce": round(ph["allreduce"], 3),
+            "source": "%d iterations after the timed region, HIP events on "
+                      "every launch" % PHASE_ITERS},
     }
     # the CPU baseline is timed on rank 0 of the N=1 run only
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

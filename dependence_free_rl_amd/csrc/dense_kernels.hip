@@ -12,6 +12,8 @@
 //                                             over rows into per-split slabs
 // One dimension may be a device-side row count (rows of this learn() batch),
 // so a launch needs no host synchronisation.
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "xh_device.h"
@@ -235,23 +237,14 @@ struct CtxOf<L, true> {
 };
 }  // namespace detail
 
-// dyn: 0 = static sizes, 1 = M is *rows, 2 = K is *rows (each <= the static
-// bound).  Split-K: blockIdx.z takes K range [z*kper, (z+1)*kper).
-template <class LA, class LB, class EP>
-__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
-                                                   int N, int K, const int *rows,
-                                                   int dyn) {
-  __shared__ float As[BK][BM + PAD];
-  __shared__ float Bs[BK][BN + PAD];
-  if (dyn == 1) M = min(M, *rows);
-  if (dyn == 2) K = min(K, *rows);
-  const int bm = blockIdx.x * BM, bn = blockIdx.y * BN;
-  if (bm >= M && dyn == 1) return;  // no rows for this tile (uniform exit)
-  const int splits = gridDim.z;
-  int kper = (K + splits - 1) / splits;
-  kper = (kper + BK - 1) / BK * BK;
-  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
-
+// One 64x64 output tile (rows bm.., columns bn..) over K range [k0, k1):
+// the waves' 32x32 accumulators (wave w: rows 32 (w & 1), columns 32 (w >> 1)).
+// Every caller that needs the GEMM's bits runs this exact chain.
+template <class LA, class LB>
+__device__ __forceinline__ f32x16 gemm_tile(const LA &la, const LB &lb, int M,
+                                            int N, int bm, int bn, int k0, int k1,
+                                            float (&As)[BK][BM + PAD],
+                                            float (&Bs)[BK][BN + PAD]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
   f32x16 acc = zero16();
@@ -318,11 +311,233 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
     for (int kk = 0; kk < BK; kk += 2)
       acc = mfma32(As[kk + h][wm * 32 + lr], Bs[kk + h][wn * 32 + lr], acc);
   }
+  return acc;
+}
+
+// dyn: 0 = static sizes, 1 = M is *rows, 2 = K is *rows (each <= the static
+// bound).  Split-K: blockIdx.z takes K range [z*kper, (z+1)*kper).
+template <class LA, class LB, class EP>
+__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EP ep, int M,
+                                                   int N, int K, const int *rows,
+                                                   int dyn) {
+  __shared__ float As[BK][BM + PAD];
+  __shared__ float Bs[BK][BN + PAD];
+  if (dyn == 1) M = min(M, *rows);
+  if (dyn == 2) K = min(K, *rows);
+  const int bm = blockIdx.x * BM, bn = blockIdx.y * BN;
+  if (bm >= M && dyn == 1) return;  // no rows for this tile (uniform exit)
+  const int splits = gridDim.z;
+  int kper = (K + splits - 1) / splits;
+  kper = (kper + BK - 1) / BK * BK;
+  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
+  const f32x16 acc = gemm_tile(la, lb, M, N, bm, bn, k0, k1, As, Bs);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
   const int n = bn + wn * 32 + lr;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = bm + wm * 32 + acc_row(r, h);
     if (m < M && n < N) ep(m, n, blockIdx.z, acc[r]);
+  }
+}
+
+// ---------------------------------------------- the value MLP, fused ----
+// The value net of the learners (full Fin -> 64 -> 32 -> 1 with relu between,
+// the value_h1 / value_h2 defaults; ppo_training.cc:19-26) in three launches
+// per update instead of nine, every output bit-identical to the layer-by-
+// layer GEMMs above: each fused phase feeds the MFMA the operand values of
+// the corresponding gemm_kernel launch in the same k order (gemm_tile itself
+// for the observation-gathering layer 0, the LDS-resident hidden tiles for
+// the others), and the same epilogue arithmetic.
+constexpr int kFV1 = 64, kFV2 = 32;
+constexpr int kHS = kFV1 + 2;  // LDS row stride of the hidden tiles: lanes
+                               // (lr, h) read row lr, column k + h -> banks
+                               // 2 lr + h, conflict-free
+struct Mlp3Fwd {
+  const float *b0, *W1, *b1, *W2, *b2;
+  float *act0, *act1, *out;
+  const int *term_list;  // non-null: rows >= term_from also write V to
+  int term_from;         // v_term[term_list[row - term_from]]
+  float *v_term;
+};
+
+// Forward, one 64-row tile per workgroup: layer 0 (gemm_tile), layer 1 and
+// layer 2 from the tile in LDS.  act0 / act1 are written for the backward.
+template <class LA, class LB>
+__global__ __launch_bounds__(256) void mlp3_forward_kernel(LA la, LB w0, Mlp3Fwd o,
+                                                           int M, int K0,
+                                                           const int *rows) {
+  __shared__ float As[BK][BM + PAD];
+  __shared__ float Bs[BK][BN + PAD];
+  __shared__ float Hs[BM][kHS];        // H1, then H2 in columns 0..31
+  __shared__ float W1s[kFV2][kHS];     // W1 [out][in]
+  __shared__ float W2s[kFV2];
+  if (rows) M = min(M, *rows);
+  const int bm = blockIdx.x * BM;
+  if (bm >= M) return;  // uniform
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
+  for (int i = tid; i < kFV2 * kFV1; i += 256) W1s[i / kFV1][i % kFV1] = o.W1[i];
+  if (tid < kFV2) W2s[tid] = o.W2[tid];
+  // layer 0: mlp_forward's first GEMM tile (its barriers also order the
+  // staging above before the reads below)
+  const f32x16 acc = gemm_tile(la, w0, M, kFV1, bm, 0, 0, K0, As, Bs);
+  {
+    const int n = wn * 32 + lr;
+    const float b = o.b0[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = wm * 32 + acc_row(r, h), m = bm + i;
+      float v = acc[r] + b;
+      v = v > 0.0f ? v : 0.0f;
+      Hs[i][n] = v;
+      if (m < M) o.act0[(size_t)m * kFV1 + n] = v;
+    }
+  }
+  __syncthreads();
+  // layer 1 (64 -> 32): the waves of output columns 0..31
+  f32x16 acc1 = zero16();
+  if (wn == 0) {
+#pragma unroll
+    for (int k = 0; k < kFV1; k += 2)
+      acc1 = mfma32(Hs[wm * 32 + lr][k + h], W1s[lr][k + h], acc1);
+  }
+  __syncthreads();  // every read of H1 done before H2 replaces it
+  if (wn == 0) {
+    const float b = o.b1[lr];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = wm * 32 + acc_row(r, h), m = bm + i;
+      float v = acc1[r] + b;
+      v = v > 0.0f ? v : 0.0f;
+      Hs[i][lr] = v;
+      if (m < M) o.act1[(size_t)m * kFV2 + lr] = v;
+    }
+  }
+  __syncthreads();
+  // layer 2 (32 -> 1): output column 0 (lanes lr == 0)
+  if (wn == 0) {
+    f32x16 acc2 = zero16();
+#pragma unroll
+    for (int k = 0; k < kFV2; k += 2)
+      acc2 = mfma32(Hs[wm * 32 + lr][k + h], lr == 0 ? W2s[k + h] : 0.0f, acc2);
+    if (lr == 0) {
+      const float b = o.b2[0];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = bm + wm * 32 + acc_row(r, h);
+        if (m < M) {
+          const float v = acc2[r] + b;
+          o.out[m] = v;
+          if (o.term_list && m >= o.term_from) o.v_term[o.term_list[m - o.term_from]] = v;
+        }
+      }
+    }
+  }
+}
+
+// Backward through the data path for one 64-row tile of transition rows:
+// value_targets_kernel's TD targets and dL/dV = V - target (square_loss_grad,
+// nn.h:548-550), then dX2 = (dV W2) * [H2 > 0] and dX1 = (dX2 W1) * [H1 > 0]
+// (the two EpReluMask GEMMs of mlp_backward, their chains: K = 1 and K = 32).
+struct Mlp3Bwd {
+  ValueArgs va;
+  float gamma;
+  float *targets;
+  const float *W1, *W2, *act0, *act1;
+  float *g2, *g1, *g0;  // dV [rows], dX2 [rows][32], dX1 [rows][64]
+};
+__global__ __launch_bounds__(256) void mlp3_backward_data_kernel(Mlp3Bwd o, int M) {
+#pragma clang fp contract(off)
+  __shared__ float G2[BM][kHS];      // dX2 tile (columns 0..31)
+  __shared__ float W1s[kFV2][kHS];   // W1 [out k][in n]
+  __shared__ float rg[BM];
+  const int bm = blockIdx.x * BM;
+  if (bm >= M) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
+  for (int i = tid; i < kFV2 * kFV1; i += 256) W1s[i / kFV1][i % kFV1] = o.W1[i];
+  if (tid < BM) {
+    const int q = bm + tid;
+    float g = 0.0f;
+    if (q < M) {
+      const int N = o.va.b.N;
+      const int done = o.va.b.done[q];
+      const float reward = done ? 0.0f : 1.0f;
+      const float vn = done ? o.va.v_term[q] : o.va.v_state[q + N];
+      const float target = reward + o.gamma * vn;
+      o.targets[q] = target;
+      g = o.va.v_state[q] - target;
+      o.g2[q] = g;
+    }
+    rg[tid] = g;
+  }
+  __syncthreads();
+  // dX2: K = 1 (k = 0 in lane half 0 of the first step; the rest of the
+  // gemm's BK = 16 slice is its zero pad, kept so the bits match)
+  if (wn == 0) {
+    const float ga = h == 0 ? rg[wm * 32 + lr] : 0.0f, gb = h == 0 ? o.W2[lr] : 0.0f;
+    f32x16 acc = mfma32(ga, gb, zero16());
+#pragma unroll
+    for (int kk = 2; kk < BK; kk += 2) acc = mfma32(0.0f, 0.0f, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = wm * 32 + acc_row(r, h), m = bm + i;
+      float v = 0.0f;
+      if (m < M) {
+        v = o.act1[(size_t)m * kFV2 + lr] > 0.0f ? acc[r] : 0.0f;
+        o.g1[(size_t)m * kFV2 + lr] = v;
+      }
+      G2[i][lr] = v;
+    }
+  }
+  __syncthreads();
+  // dX1: K = 32, every wave (64 x 64)
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < kFV2; k += 2)
+    acc = mfma32(G2[wm * 32 + lr][k + h], W1s[k + h][wn * 32 + lr], acc);
+  const int n = wn * 32 + lr;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = bm + wm * 32 + acc_row(r, h);
+    if (m < M)
+      o.g0[(size_t)m * kFV1 + n] = o.act0[(size_t)m * kFV1 + n] > 0.0f ? acc[r] : 0.0f;
+  }
+}
+
+// The three weight-gradient GEMMs of mlp_backward ([dW | db] = dY^T [X | 1],
+// split-K over the rows into slabs) in one launch: blockIdx.x enumerates
+// layer 2's tile, layer 1's two and layer 0's n0 tiles, blockIdx.z the split.
+template <class LB0, class EP0>
+__global__ __launch_bounds__(256) void mlp3_weight_grad_kernel(
+    ColMajor d2, RowsOnes x2, EpSlab e2, ColMajor d1, RowsOnes x1, EpSlab e1,
+    ColMajor d0, LB0 x0, EP0 e0, int N0, int K) {
+  __shared__ float As[BK][BM + PAD];
+  __shared__ float Bs[BK][BN + PAD];
+  const int splits = gridDim.z;
+  int kper = (K + splits - 1) / splits;
+  kper = (kper + BK - 1) / BK * BK;
+  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
+  auto out = [&](const f32x16 &acc, int M, int N, int bn, auto &ep) {
+    const int n = bn + wn * 32 + lr;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = wm * 32 + acc_row(r, h);
+      if (m < M && n < N) ep(m, n, blockIdx.z, acc[r]);
+    }
+  };
+  const int b = blockIdx.x;  // uniform
+  if (b == 0) {
+    out(gemm_tile(d2, x2, 1, kFV2 + 1, 0, 0, k0, k1, As, Bs), 1, kFV2 + 1, 0, e2);
+  } else if (b < 3) {
+    const int bn = (b - 1) * BN;
+    out(gemm_tile(d1, x1, kFV2, kFV1 + 1, 0, bn, k0, k1, As, Bs), kFV2, kFV1 + 1, bn, e1);
+  } else {
+    const int bn = (b - 3) * BN;
+    out(gemm_tile(d0, x0, kFV1, N0, 0, bn, k0, k1, As, Bs), kFV1, N0, bn, e0);
   }
 }
 
@@ -366,8 +581,49 @@ __global__ void reduce_w0_kernel(const float *W, int out, int B, int D,
   }
 }
 
+bool value_fused(const MlpArgs &a) {
+  const char *e = std::getenv("XH_VALUE_KERNEL");
+  if (e && std::strcmp(e, "gemm") == 0) return false;
+  return a.nlayers == 3 && a.w[1] == dense::kFV1 && a.w[2] == dense::kFV2 &&
+         a.w[3] == 1;
+}
+
+static hipError_t mlp3_forward(const MlpArgs &a, hipStream_t s) {
+  using namespace dense;
+  const int in = a.w[0];
+  const float *W0 = a.params;
+  const int o1 = layer_offset(a.w, 1), o2 = layer_offset(a.w, 2);
+  Mlp3Fwd o{W0 + kFV1 * in, a.params + o1, a.params + o1 + kFV2 * kFV1,
+            a.params + o2, a.params + o2 + kFV2, a.act[0], a.act[1], a.act[2],
+            a.v_term ? a.term_list : nullptr, a.term_from, a.v_term};
+  const dim3 grid((a.max_rows + BM - 1) / BM);
+  auto run = [&](auto la, const RowMajor &w0, int K0) {
+    hipLaunchKernelGGL((mlp3_forward_kernel<decltype(la), RowMajor>), grid,
+                       dim3(256), 0, s, la, w0, o, a.max_rows, K0, a.rows);
+    return hipGetLastError();
+  };
+  if (a.w0red) {
+    const int K = a.env.B * a.env.D + a.env.D;
+    int nb = (kFV1 * K + 255) / 256;
+    nb = nb > 1024 ? 1024 : nb;
+    hipLaunchKernelGGL(reduce_w0_kernel, dim3(nb), dim3(256), 0, s, W0, kFV1,
+                       a.env.B, a.env.D, a.w0red);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const RowMajor wr{a.w0red, K};
+    if (a.env.D == 1) return run(obs_loader<ObsRedA<1>>(a), wr, K);
+    if (a.env.D == 2) return run(obs_loader<ObsRedA<2>>(a), wr, K);
+    return run(obs_loader<ObsRedA<3>>(a), wr, K);
+  }
+  const RowMajor wt{W0, in};
+  if (a.env.D == 1) return run(obs_loader<ObsA<1>>(a), wt, in);
+  if (a.env.D == 2) return run(obs_loader<ObsA<2>>(a), wt, in);
+  return run(obs_loader<ObsA<3>>(a), wt, in);
+}
+
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
   using namespace dense;
+  if (value_fused(a)) return mlp3_forward(a, s);
   hipError_t e = hipSuccess;
   for (int l = 0; l < a.nlayers && e == hipSuccess; ++l) {
     const int in = a.w[l], out = a.w[l + 1];
@@ -409,6 +665,9 @@ hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
       e = gemm(la, wt, ep, a.max_rows, out, in, a.rows, a.rows ? 1 : 0, 1, s);
     }
   }
+  if (e == hipSuccess && a.v_term && a.term_list)
+    e = launch_scatter_list(a.term_list, a.term_n, a.act[a.nlayers - 1] + a.term_from,
+                            a.v_term, a.max_rows - a.term_from, s);
   return e;
 }
 
@@ -461,6 +720,56 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
     }
   }
   return e;
+}
+
+hipError_t value_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
+                          float *targets, float *slab, int stride, int splits,
+                          hipStream_t s) {
+  using namespace dense;
+  if (!value_fused(a)) {
+    ValueArgs v = va;
+    v.row_g = a.grad[a.nlayers - 1];
+    hipError_t e = launch_value_targets(v, gamma, targets, s);
+    return e != hipSuccess ? e : mlp_backward(a, slab, stride, splits, s);
+  }
+  const int M = a.max_rows, in = a.w[0];
+  const int o1 = layer_offset(a.w, 1), o2 = layer_offset(a.w, 2);
+  Mlp3Bwd o{va, gamma, targets, a.params + o1, a.params + o2, a.act[0],
+            a.act[1], a.grad[2], a.grad[1], a.grad[0]};
+  hipLaunchKernelGGL(mlp3_backward_data_kernel, dim3((M + BM - 1) / BM), dim3(256),
+                     0, s, o, M);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const ColMajor d2{a.grad[2], 1}, d1{a.grad[1], kFV2}, d0{a.grad[0], kFV1};
+  const RowsOnes x2{a.act[1], kFV2, kFV2}, x1{a.act[0], kFV1, kFV1};
+  const EpSlab e2{slab, stride, o2, o2 + kFV2, kFV2};
+  const EpSlab e1{slab, stride, o1, o1 + kFV2 * kFV1, kFV1};
+  const int sp = splits < 1 ? 1 : splits;
+  auto run = [&](auto x0, auto e0, int N0) {
+    const dim3 grid(3 + (N0 + BN - 1) / BN, 1, sp);
+    hipLaunchKernelGGL((mlp3_weight_grad_kernel<decltype(x0), decltype(e0)>), grid,
+                       dim3(256), 0, s, d2, x2, e2, d1, x1, e1, d0, x0, e0, N0, M);
+    return hipGetLastError();
+  };
+  if (a.w0red) {
+    const int K = a.env.B * a.env.D + a.env.D;
+    const EpSlabRed er{slab, stride, 0, kFV1 * in, in, a.env.B, a.env.D};
+    auto go = [&](auto lb) {
+      lb.ncol = K;
+      return run(lb, er, K + 1);
+    };
+    if (a.env.D == 1) return go(obs_loader<ObsRedOnesB<1>>(a));
+    if (a.env.D == 2) return go(obs_loader<ObsRedOnesB<2>>(a));
+    return go(obs_loader<ObsRedOnesB<3>>(a));
+  }
+  const EpSlab es{slab, stride, 0, kFV1 * in, in};
+  auto go = [&](auto lb) {
+    lb.ncol = in;
+    return run(lb, es, in + 1);
+  };
+  if (a.env.D == 1) return go(obs_loader<ObsOnesB<1>>(a));
+  if (a.env.D == 2) return go(obs_loader<ObsOnesB<2>>(a));
+  return go(obs_loader<ObsOnesB<3>>(a));
 }
 
 // ------------------------------------------------ model::eval on device --

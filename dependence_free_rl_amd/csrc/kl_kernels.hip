@@ -105,10 +105,95 @@ __global__ __launch_bounds__(kELB) void end_write_kernel(EndListArgs a,
       if (a.done[(size_t)t * a.N + e]) a.end_list[pos++] = t * a.N + e;
 }
 
+// The same list in one launch of one workgroup for N <= 1024 C, N % 4 == 0:
+// thread i owns envs [i C, (i+1) C), reads their done bytes as 32-bit words
+// (independent loads), keeps one count per env in registers, one block-wide
+// exclusive scan of the thread totals, then writes its envs' entries (t outer,
+// so each env's entries stay in t order at their env-major positions).
+template <int C>
+__global__ __launch_bounds__(1024) void end_list_kernel(EndListArgs a) {
+  static_assert(C % 4 == 0, "whole words");
+  __shared__ int sc[1024];
+  __shared__ int osum[1024];
+  const int tid = threadIdx.x, e0 = tid * C;
+  int cnt[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) cnt[i] = 0;
+  int open = 0;
+  auto word = [&](int t, int w) -> unsigned {
+    return e0 + 4 * w < a.N
+               ? reinterpret_cast<const unsigned *>(a.done + (size_t)t * a.N + e0)[w]
+               : 0u;
+  };
+  for (int t = 0; t < a.T; ++t)
+#pragma unroll
+    for (int w = 0; w < C / 4; ++w) {
+      const unsigned v = word(t, w);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) cnt[4 * w + b] += ((v >> (8 * b)) & 0xffu) != 0;
+    }
+#pragma unroll
+  for (int w = 0; w < C / 4; ++w) {
+    const unsigned v = word(a.T - 1, w);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      open += e0 + 4 * w + b < a.N && ((v >> (8 * b)) & 0xffu) == 0;
+  }
+  int total = 0;
+#pragma unroll
+  for (int i = 0; i < C; ++i) total += cnt[i];
+  sc[tid] = total;
+  osum[tid] = open;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int u = tid >= off ? sc[tid - off] : 0;
+    __syncthreads();
+    sc[tid] += u;
+    __syncthreads();
+  }
+  for (int off = 512; off > 0; off >>= 1) {
+    if (tid < off) osum[tid] += osum[tid + off];
+    __syncthreads();
+  }
+  int pos[C];
+  {
+    int p = sc[tid] - total;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      pos[i] = p;
+      p += cnt[i];
+    }
+  }
+  for (int t = 0; t < a.T; ++t)
+#pragma unroll
+    for (int w = 0; w < C / 4; ++w) {
+      const unsigned v = word(t, w);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((v >> (8 * b)) & 0xffu) a.end_list[pos[4 * w + b]++] = t * a.N + e0 + 4 * w + b;
+    }
+  if (tid == 0) {
+    *a.n_end = sc[1023];
+    *a.n_open = osum[0];
+    if (a.rows_out) *a.rows_out = a.rows_base + sc[1023];
+  }
+}
+
 int end_list_scratch_ints(int N) { return 2 * ((N + kELB - 1) / kELB); }
 
 hipError_t launch_end_list(const EndListArgs &a, int *scratch,
                                hipStream_t s) {
+  if (a.N % 4 == 0 && a.N <= 1024 * 32) {
+    if (a.N <= 1024 * 4)
+      hipLaunchKernelGGL(end_list_kernel<4>, dim3(1), dim3(1024), 0, s, a);
+    else if (a.N <= 1024 * 8)
+      hipLaunchKernelGGL(end_list_kernel<8>, dim3(1), dim3(1024), 0, s, a);
+    else if (a.N <= 1024 * 16)
+      hipLaunchKernelGGL(end_list_kernel<16>, dim3(1), dim3(1024), 0, s, a);
+    else
+      hipLaunchKernelGGL(end_list_kernel<32>, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+  }
   const int nblk = (a.N + kELB - 1) / kELB;
   hipLaunchKernelGGL(end_count_kernel, dim3(nblk), dim3(kELB), 0, s, a, scratch);
   hipLaunchKernelGGL(end_base_kernel, dim3(1), dim3(1024), 0, s, a, scratch,

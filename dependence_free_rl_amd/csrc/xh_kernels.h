@@ -193,12 +193,28 @@ struct MlpArgs {
   const float *params;  // flat model::parameters() layout
   float *act[3];
   float *grad[3];
+  // optional with term_list: the output of row term_from + j also goes to
+  // v_term[term_list[j]] for j < *term_n (the terminal views' values onto
+  // their transition rows)
+  float *v_term;
+  const int *term_n;
 };
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s);
 // Weight gradients of every layer into slab[split] (flat layout), data
 // gradients down to layer 1 (layer 0 gets no backward, nn.h:516-526).
 hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
                         hipStream_t s);
+// update_value_model's backward (policy_gradient.h:196-218) over the
+// a.max_rows transition rows: TD targets and dL/dV = V - target
+// (value_targets_kernel, into targets and a.grad[last]), then mlp_backward.
+// The Fin -> 64 -> 32 -> 1 value net runs fused (two launches, the same
+// bits) unless XH_VALUE_KERNEL=gemm.
+hipError_t value_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
+                          float *targets, float *slab, int stride, int splits,
+                          hipStream_t s);
+// true: mlp_forward / value_backward run a fused (the Fin -> 64 -> 32 -> 1
+// shape, no XH_VALUE_KERNEL=gemm)
+bool value_fused(const MlpArgs &a);
 
 // model::eval of a described layer chain (dense_kernels.hip, xh_model_eval).
 enum LayerKind { kLayerFull = 0, kLayerConv1d = 1, kLayerRelu = 2,

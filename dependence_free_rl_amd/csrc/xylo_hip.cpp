@@ -130,7 +130,7 @@ struct xh_trainer {
   std::vector<char> bins_wide;
   // what the last rollout step / policy epoch launched (xh_trainer_kernel_info)
   xh::KernelInfo last_rollout, last_train;
-  bool timing = false;
+  int timing = 0;  // 0 off, 1 every launch, XH_TIMING_TRAIN policy_train only
   bool counted = false;  // holds a reference on ctx
   std::vector<timed_event> events;
   std::vector<hipEvent_t> event_pool;  // recycled by reset_timing
@@ -222,7 +222,9 @@ template <class F>
 int timed(xh_trainer *t, const char *name, F &&launch) {
   hipStream_t s = t->ctx->stream;
   timed_event ev;
-  if (t->timing) {
+  const bool rec = t->timing == 1 ||
+                   (t->timing == XH_TIMING_TRAIN && std::strcmp(name, "policy_train") == 0);
+  if (rec) {
     ev.name = name;
     HIPCHK(pooled_event(t, &ev.start));
     HIPCHK(pooled_event(t, &ev.stop));
@@ -231,7 +233,7 @@ int timed(xh_trainer *t, const char *name, F &&launch) {
   hipError_t e = launch();
   if (e != hipSuccess)
     return fail(XH_ERR_HIP, "launch %s: %s", name, hipGetErrorString(e));
-  if (t->timing) {
+  if (rec) {
     HIPCHK(hipEventRecord(ev.stop, s));
     t->events.push_back(ev);
   }
@@ -665,23 +667,21 @@ int do_learn(xh_trainer *t) {
   // terminal views E_t of the ended transitions in one batch (NS + n_end
   // rows, a device count), TD targets and dL/dV = V - target on the
   // transition rows (end rows have zero gradient), backward, one step
+  // (the terminal views' values also land on their transition rows, v_term)
   xh::MlpArgs vm = value_mlp(t, NS + NT, t->v_state0);
   vm.rows = t->vrows;
   vm.term_list = t->end_list;
+  vm.v_term = t->v_term;
+  vm.term_n = t->n_end;
   CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
-  CHK(timed(t, "value", [&]() {
-    return xh::launch_scatter_list(t->end_list, t->n_end, t->v_state0 + NS,
-                                   t->v_term, NT, s);
-  }));
   vm.rows = nullptr;
   vm.term_list = nullptr;
+  vm.v_term = nullptr;
   va.v_state = t->v_state0;
-  CHK(timed(t, "value", [&]() {
-    return xh::launch_value_targets(va, c.gamma, t->targets, s);
-  }));
   vm.max_rows = NT;
   CHK(timed(t, "value", [&]() {
-    return xh::mlp_backward(vm, t->vslab, t->vslab_stride, t->vslab_n, s);
+    return xh::value_backward(vm, va, c.gamma, t->targets, t->vslab,
+                              t->vslab_stride, t->vslab_n, s);
   }));
   // the reduced layer 0 writes bin 0's item columns only (EpSlabRed)
   const xh::SlabAlias al =
@@ -1828,7 +1828,9 @@ int xh_trainer_seed_streams(xh_trainer *t, uint32_t x) {
 
 int xh_trainer_set_timing(xh_trainer *t, int on) {
   if (!t) return fail(XH_ERR_INVALID, "null trainer");
-  t->timing = on != 0;
+  if (on < 0 || on > XH_TIMING_TRAIN)
+    return fail(XH_ERR_INVALID, "set_timing: mode %d (0, 1 or XH_TIMING_TRAIN)", on);
+  t->timing = on;
   return XH_OK;
 }
 
@@ -1851,11 +1853,17 @@ int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap) {
     if (!t || !buf || cap == 0) return fail(XH_ERR_INVALID, "null arg");
     const std::string js = "{\"rollout_step\": " + kernel_json(t->last_rollout) +
                            ", \"policy_train\": " + kernel_json(t->last_train) +
-                           ", \"train_grid\": " + std::to_string(t->pslab_n) +
+                           ", \"value\": \"" +
+                           (t->cfg.algo != XH_PG &&
+                                    xh::value_fused(value_mlp(t, 0, nullptr))
+                                ? std::string("mlp3_fused")
+                                : std::string("gemm")) +
+                           "\", \"train_grid\": " + std::to_string(t->pslab_n) +
                            ", \"train_grid_cap\": " +
                            std::to_string(t->cfg.train_grid_cap) +
                            ", \"overrides\": {" + env_json("XH_TRAIN_KERNEL") +
-                           ", " + env_json("XH_ROLLOUT_KERNEL") + "}}";
+                           ", " + env_json("XH_ROLLOUT_KERNEL") + ", " +
+                           env_json("XH_VALUE_KERNEL") + "}}";
     if (js.size() + 1 > cap)
       return fail(XH_ERR_INVALID, "kernel_info: %zu bytes needed", js.size() + 1);
     std::memcpy(buf, js.c_str(), js.size() + 1);

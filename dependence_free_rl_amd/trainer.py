@@ -496,7 +496,10 @@ class Trainer:
 
     # ------------------------------------------------------------ timing --
     def set_timing(self, on):
-        check(_lib.lib.xh_trainer_set_timing(self.h, 1 if on else 0))
+        """on: False / True (every launch) / "train" (the policy train
+        launches only: XH_TIMING_TRAIN)."""
+        mode = 2 if on == "train" else (1 if on else 0)
+        check(_lib.lib.xh_trainer_set_timing(self.h, mode))
 
     def reset_timing(self):
         check(_lib.lib.xh_trainer_reset_timing(self.h))

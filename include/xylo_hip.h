@@ -430,7 +430,11 @@ int xh_trainer_forget(xh_trainer *t);
  * foreign-language binding can check its mirror of them. */
 size_t xh_struct_size(const char *name);
 
-/* Kernel timing with HIP events on the trainer's stream (off by default). */
+/* Kernel timing with HIP events on the trainer's stream (off by default).
+ * on = 1: every launch (the phase breakdown; the events themselves cost
+ * about 2 us per launch of wall time); on = XH_TIMING_TRAIN (2): the policy
+ * train launches only (the dominant kernel's average duration, nearly free). */
+#define XH_TIMING_TRAIN 2
 int xh_trainer_set_timing(xh_trainer *t, int on);
 /* name: "rollout_step" | "policy_train" | "value" | "reduce_sgd" | "allreduce"
  * Returns accumulated milliseconds and launch count since the last reset. */
@@ -440,7 +444,7 @@ int xh_trainer_reset_timing(xh_trainer *t);
 /* Which kernels the trainer's last rollout step and last policy epoch
  * launched, and their arithmetic, as a JSON object written NUL-terminated
  * into buf[cap]:
- *   {"rollout_step": K, "policy_train": K, "train_grid": G,
+ *   {"rollout_step": K, "policy_train": K, "value": V, "train_grid": G,
  *    "train_grid_cap": C, "overrides": {...}}
  *   K = {"kernel": name | null (not launched yet),
  *        "math": one of
@@ -457,11 +461,13 @@ int xh_trainer_reset_timing(xh_trainer *t);
  *        "bf16_products_per_f32_product": p for "bf16_split", else null,
  *        "peak_tflops": the dense MFMA peak of that arithmetic on MI355X
  *        (2500 / p, or 157.3)}
+ *   V = "mlp3_fused" (the Fin -> 64 -> 32 -> 1 value net in three launches
+ *   per update) or "gemm" (layer by layer, other widths),
  *   G = the train grid (workgroups, = gradient slabs), C = xh_config
  *   train_grid_cap.
  * "overrides" lists the diagnostic environment variables that steer kernel
- * selection (XH_TRAIN_KERNEL, XH_ROLLOUT_KERNEL) with their values, or null
- * when unset. */
+ * selection (XH_TRAIN_KERNEL, XH_ROLLOUT_KERNEL, XH_VALUE_KERNEL) with their
+ * values, or null when unset. */
 int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap);
 
 #ifdef __cplusplus

@@ -70,7 +70,8 @@ def test_roofline_math_comes_from_the_library(bench):
     assert "kernel_info()" in src and "train_split_active" not in src
 
 
-@pytest.mark.parametrize("var", ["XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL"])
+@pytest.mark.parametrize("var", ["XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL",
+                                 "XH_VALUE_KERNEL"])
 def test_bench_refuses_kernel_overrides(var):
     """A kernel-selection override in the environment stops the bench before
     it touches the device, unless --allow-kernel-override is given."""

@@ -229,7 +229,9 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
     else:
         assert kt["math"] == "f32_mfma" and kt["peak_tflops"] == 157.3
         assert kt["kernel"].startswith("policy_train")
-    assert k["overrides"] == {"XH_TRAIN_KERNEL": None, "XH_ROLLOUT_KERNEL": None}
+    assert k["overrides"] == {"XH_TRAIN_KERNEL": None, "XH_ROLLOUT_KERNEL": None,
+                            "XH_VALUE_KERNEL": None}
+    assert k["value"] == "mlp3_fused"
     tr.close()
     if train:
         monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
