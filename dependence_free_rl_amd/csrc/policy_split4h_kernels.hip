@@ -26,6 +26,30 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Phase stamps (trace build, tools/build_trace4h.sh: -DXH_DIAG_TRACE=1, run
+// with XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
+// workgroups records the cycle counter at 0 X start, 1 layer 2 (+ group j's
+// VALU) done, 2 partial logits written, 3 after the X barrier, 4 dW2 / dH1
+// blocks done, 5 dW1 tail done, 6 after the Y barrier (7 = 6) for groups
+// j < kTraceGroups - 1; trace group kTraceGroups - 1 holds the kernel-level
+// stamps 0 start, 1 pipeline filled, 2 groups done, 3 slab written.
+#ifndef XH_DIAG_TRACE
+#define XH_DIAG_TRACE 0
+#endif
+#if XH_DIAG_TRACE
+#define S4H_STAMP(a, gi, w, lane, slot)                                         \
+  do {                                                                        \
+    if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups &&      \
+        (lane) == 0)                                                          \
+      (a).trace[((blockIdx.x * kTraceGroups + (gi)) * 8 + (w)) * kTraceSlots + \
+                (slot)] = clock64();                                          \
+  } while (0)
+#else
+#define S4H_STAMP(a, gi, w, lane, slot) \
+  do {                                  \
+  } while (0)
+#endif
+
 namespace xh {
 namespace s4h {
 
@@ -50,7 +74,8 @@ constexpr int F_XP = F_X + 3 * 64;       // [3 slots][16 li][4 rt]
 constexpr int F_IT = F_XP + 3 * 64;      // [3 slots][2 envs] item is item_a (+ pad)
 constexpr int F_REC = F_IT + 8;          // [3 slots][2 envs][action, pold, adv, -]
 constexpr int F_SC = F_REC + 3 * 8;      // [16] the scales' reduction
-constexpr int F_END = F_SC + 16;
+constexpr int F_W3G = F_SC + 16;         // [64] w3 (the slab write-out's)
+constexpr int F_END = F_W3G + kH;
 constexpr size_t kLds = L_F + sizeof(float) * F_END;
 static_assert(2 * kLds <= 160 * 1024, "LDS: two workgroups per CU");
 static_assert(F_REC % 4 == 0 && F_GW % 4 == 0 && F_GP % 4 == 0 && F_X % 4 == 0 &&
@@ -153,6 +178,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int l = tid & 63, G = l >> 4, li = l & 15;
+  constexpr int kKG = kTraceGroups - 1;  // the kernel-level stamps' group
+  S4H_STAMP(a, kKG, w, l, 0);
   const int ngroups = a.b.T * a.b.N / 2;  // 64-row groups of two envs
   const int J = (int)blockIdx.x < ngroups
                     ? (ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x
@@ -165,8 +192,51 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     return (size_t)((int)blockIdx.x + min(j, J - 1) * gstep);
   };
 
-  // ---- prologue: the scales (every workgroup the same), small parameters,
-  // the W2 / W2' fragments of tile w as f16 pairs
+  // wave 0 stages group j+2 during X(j): branch-free loads at its start
+  // (lane = row: its bin; lanes 0-2 / 3-5 env A's / B's action, old
+  // probability and advantage, lanes 6 / 7 their items), the stores late
+  struct Raw {
+    int bi, rec;
+  };
+  // (every wave loads -- the loads are tiny -- and only wave 0 stores: no
+  // branch around the loads, whose results then stay in flight until the
+  // store; the byte is sign-extended there, and the record address is chosen
+  // by selects, not branches)
+  auto stage_load = [&](int j) {
+    const size_t g = gindex(j);
+    int lo = l;
+    asm volatile("" : "+v"(lo));
+    const int bins = (int)*reinterpret_cast<const unsigned char *>(a.b.bins + g * 64 + lo);
+    const size_t ti = 2 * g + (l >= 3 && l != 6);
+    const int k = l % 3;
+    const unsigned long long p0 = (unsigned long long)(a.b.action + ti);
+    const unsigned long long p1 = (unsigned long long)(a.b.pold + ti);
+    const unsigned long long p2 = (unsigned long long)(a.adv + ti);
+    const unsigned long long p3 = (unsigned long long)(a.b.items + (2 * g + (l & 1)) * 4);
+    unsigned long long pa = k == 1 ? p1 : p2;
+    pa = k == 0 ? p0 : pa;
+    pa = l >= 6 ? p3 : pa;
+    return Raw{bins, *reinterpret_cast<const int *>(pa)};
+  };
+  // ---- prologue: every global load first (the scales' inputs, the small
+  // parameters, this lane's W2 / W2' fragment values), then the scales
+  // (every workgroup the same), then the f16 pairs of tile w
+  const int rdb0 = rd_base(G, li);
+  const Raw raw0 = stage_load(0), raw1 = stage_load(1);  // groups 0, 1's rows
+  float4 wraw[2][2];   // W2[16 w + li][32 s + 8 G ..]
+  float draw[2][8];    // W2[32 s + 8 G + j][16 w + li] * w3[32 s + 8 G + j]
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float4 *src = reinterpret_cast<const float4 *>(
+        P + PL.oW2() + (16 * w + li) * kH + 32 * s + 8 * G);
+    wraw[s][0] = src[0];
+    wraw[s][1] = src[1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = 32 * s + 8 * G + j, col = 16 * w + li;
+      draw[s][j] = P[PL.oW2() + o * kH + col] * P[PL.ow3() + o];
+    }
+  }
   {
     float mw = 0.0f, md = 0.0f, mh = 0.0f;
     {
@@ -187,9 +257,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     }
     if (tid < kH) {
       const float wv = P[PL.oW1() + tid * kF0 + kD];
-      const float ba = P[PL.ob1() + tid] + wv * ((float)a.env.item_a[0] / (float)kCapacity);
-      const float bb = P[PL.ob1() + tid] + wv * ((float)a.env.item_b[0] / (float)kCapacity);
-      mh = fabsf(P[PL.oW1() + tid * kF0]) + fmaxf(fabsf(ba), fabsf(bb));
+      const float w0v = P[PL.oW1() + tid * kF0];
+      const float b1 = P[PL.ob1() + tid];
+      const float ba = b1 + wv * ((float)a.env.item_a[0] / (float)kCapacity);
+      const float bb = b1 + wv * ((float)a.env.item_b[0] / (float)kCapacity);
+      mh = fabsf(w0v) + fmaxf(fabsf(ba), fabsf(bb));
+      // the small parameters that need no scale
+      lf[F_W1T + tid] = w0v;
+      lf[F_B1F + tid] = ba;
+      lf[F_B1F + kH + tid] = bb;
+      lf[F_W3G + tid] = P[PL.ow3() + tid];
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -214,31 +291,21 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       lf[F_SC + 12] = f16_scale_for(MW);  // S_W
       lf[F_SC + 13] = f16_scale_for(MD);  // S_D
       lf[F_SC + 14] = f16_scale_for(MH);  // S_H
+      lf[F_B3] = P[PL.ob3()];
     }
     __syncthreads();
   }
   const float SW = lf[F_SC + 12], SD = lf[F_SC + 13], SH = lf[F_SC + 14];
   const float S2 = SW * SH;  // layer 2's pre-activations are in units of S2
-  for (int i = tid; i < kH; i += kThreads) {
-    lf[F_W1T + i] = P[PL.oW1() + i * kF0];
-    lf[F_B2 + i] = P[PL.ob2() + i] * S2;
-    lf[F_W3 + i] = P[PL.ow3() + i] * (1.0f / S2);
+  if (tid < kH) {
+    lf[F_B2 + tid] = P[PL.ob2() + tid] * S2;
+    lf[F_W3 + tid] = lf[F_W3G + tid] * (1.0f / S2);
   }
-  for (int e = tid; e < 2 * kH; e += kThreads) {
-    const int it = e / kH, u = e - it * kH;
-    const int *item = it == 0 ? a.env.item_a : a.env.item_b;
-    lf[F_B1F + e] = P[PL.ob1() + u] +
-                    P[PL.oW1() + u * kF0 + kD] * ((float)item[0] / (float)kCapacity);
-  }
-  if (tid == 0) lf[F_B3] = P[PL.ob3()];
   f16x8 wl[2][2], wd[2][2];
-  const int rdb0 = rd_base(G, li);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const float4 *src = reinterpret_cast<const float4 *>(
-        P + PL.oW2() + (16 * w + li) * kH + 32 * s + 8 * G);
-    const float4 v0 = src[0], v1 = src[1];
-    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const float v[8] = {wraw[s][0].x, wraw[s][0].y, wraw[s][0].z, wraw[s][0].w,
+                        wraw[s][1].x, wraw[s][1].y, wraw[s][1].z, wraw[s][1].w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       _Float16 x0, x1;
@@ -248,9 +315,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int o = 32 * s + 8 * G + j, col = 16 * w + li;
       _Float16 x0, x1;
-      split2h((P[PL.oW2() + o * kH + col] * P[PL.ow3() + o]) * SD, x0, x1);
+      split2h(draw[s][j] * SD, x0, x1);
       wd[s][0][j] = x0;
       wd[s][1][j] = x1;
     }
@@ -269,27 +335,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float accB3 = 0.0f, w0 = 0.0f, sa = 0.0f, sb = 0.0f;
 
-  // wave 0 stages group j+2 during X(j): branch-free loads at its start
-  // (lane = row: its bin; lanes 0-2 / 3-5 env A's / B's action, old
-  // probability and advantage, lanes 6 / 7 their items), the stores late
-  struct Raw {
-    int bi, rec;
-  };
-  auto stage_load = [&](int j) {
-    const size_t g = gindex(j);
-    int lo = l;
-    asm volatile("" : "+v"(lo));
-    const int bins = (int)*reinterpret_cast<const signed char *>(a.b.bins + g * 64 + lo);
-    const size_t ti = 2 * g + (l >= 3 && l != 6);
-    const int k = l % 3;
-    const int *src = l >= 6   ? reinterpret_cast<const int *>(a.b.items + (2 * g + (l & 1)) * 4)
-                     : k == 0 ? a.b.action + ti
-                     : k == 1 ? reinterpret_cast<const int *>(a.b.pold + ti)
-                              : reinterpret_cast<const int *>(a.adv + ti);
-    return Raw{bins, *src};
-  };
   auto stage_store = [&](const Raw &r, int s) {
-    const float x = (float)r.bi / (float)kCapacity;
+    const float x = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
     lf[F_X + s * 64 + l] = x;
     lf[F_XP + s * 64 + 4 * (l & 15) + (l >> 4)] = x;
     const int itA = __builtin_amdgcn_readlane(r.rec, 6);
@@ -386,8 +433,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   f32x4 pre_cur[4];
   Raw raw = {0, 0};
   if (w == 0) {
-    stage_store(stage_load(0), 0);
-    stage_store(stage_load(1), 1);
+    stage_store(raw0, 0);
+    stage_store(raw1, 1);
   }
   __syncthreads();
   layer1_all(0, stb0);
@@ -397,12 +444,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   __syncthreads();
   layer1_all(1, stb0);
   __syncthreads();
+  S4H_STAMP(a, kKG, w, l, 1);
 
   for (int j = 0; j < J; ++j) {
+    const int gj = j < kKG ? j : kTraceGroups;  // stamped groups
+    S4H_STAMP(a, gj, w, l, 0);
     const int cs = j % 3, ns = (j + 2) % 3;  // slots of groups j and j + 2
     int rdb = rdb0, trm0 = trm00, trm1 = trm10, stb = stb0;
     asm volatile("" : "+v"(rdb), "+v"(trm0), "+v"(trm1), "+v"(stb), "+s"(gstep));
-    if (w == 0) raw = stage_load(j + 2);
+    raw = stage_load(j + 2);
     const float *xim = lf + F_X + cs * 64;
     const float w1a = lf[F_W1T + 16 * w + li];  // T layout: feature 16 w + li
 
@@ -474,12 +524,23 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) hT[h][jj] = relu(fmaf(gx0[h][jj], w1a, b1tA));
       } else if (k >= 8 && k < 12) {
-        // dW3 / db2 of r-tile rt (pre-activations in units of S2)
+        // r-tile rt: the relu masks -> the bf16 and f16 mask images, dW3 / db2
+        // (pre-activations in units of S2) from the same mask bits
         const int rt = k - 8;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        unsigned m[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
+        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
+        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
+        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
+                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
+        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
+        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float v = pre_cur[rt][jj];
-          const float gm = gr4[rt] * (float)relu_bit(v);
+          const float gm = gr4[rt] * (float)m[jj];
           accW3[jj] = fmaf(gm, v, accW3[jj]);
           accB2[jj] += gm;
         }
@@ -494,19 +555,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
           bq0[1][4 * h + jj] = p1;
           bq0[2][4 * h + jj] = p2;
         }
-      } else if (k >= 16 && k < 20) {
-        // the relu masks of r-tile k - 16 -> the bf16 and f16 mask images
-        const int rt = k - 16;
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-        unsigned m[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
-        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
-        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
-        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
-                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
-        st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
       } else if (k == 20) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 22) {
@@ -515,8 +563,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     };
     f32x4 pre_nx[4];
     layer2(rdb, pre_nx, xtask);
+    S4H_STAMP(a, gj, w, l, 1);
     partials(pre_nx, w3, (j + 1) & 1);
+    S4H_STAMP(a, gj, w, l, 2);
     __syncthreads();
+    S4H_STAMP(a, gj, w, l, 3);
 
     // ================= Y(j): dW2 / dH1 of group j with VALU of j, j+2 =====
     // 16 blocks: b < 4 dW2 of K-step 0 (ot = b), three bf16 MFMAs; 4 <= b <
@@ -549,8 +600,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       // 1 env A, 2, 3 env B)
       auto dw1 = [&](int jj, int rt) {
         const int q = rt & 1;
-        const float tT = fmaf(dx0[jj], w1a, rt < 2 ? b1tA : b1tB);
-        const float d = tT > 0.0f ? dh[q][jj] * dgg[jj] : 0.0f;
+        // relu'(layer 1) from the T-layout H1 values of g (x) H1 (the same
+        // rows: hT env A's r-tiles 0, 1, hT1 env B's 2, 3)
+        const float hv = rt == 0 ? hT[0][jj] : rt == 1 ? hT[1][jj] : rt == 2 ? hT1[0][jj] : hT1[1][jj];
+        const float d = hv > 0.0f ? dh[q][jj] * dgg[jj] : 0.0f;
         if (rt < 2)
           sgA += d;
         else
@@ -643,6 +696,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
         FENCE();
         A_c = A_n;
       }
+      S4H_STAMP(a, gj, w, l, 4);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) dw1(jj, 3);  // the last r-tile's
       if (iaA)
@@ -654,14 +708,18 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       else
         sb += sgB;
     }
+    S4H_STAMP(a, gj, w, l, 5);
     __syncthreads();
+    S4H_STAMP(a, gj, w, l, 6);
+    S4H_STAMP(a, gj, w, l, 7);
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];
   }
+  S4H_STAMP(a, kKG, w, l, 2);
 
   // ---------------------------------------------------- slab write-out ----
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
-  const float *w3g = P + PL.ow3();
+  const float *w3g = lf + F_W3G;
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
@@ -702,6 +760,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       slab[PL.ob1() + i] = va + vb;
     }
   }
+  S4H_STAMP(a, kKG, w, l, 3);
 }
 #undef FENCE
 
