@@ -221,6 +221,10 @@ def main():
     ap.add_argument("--allow-kernel-override", action="store_true",
                     help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL / XH_VALUE_KERNEL are "
                          "set (A/B measurements; the line records them)")
+    ap.add_argument("--algo", choices=("ppo", "klppo", "ac"), default=None,
+                    help="learner on the config's shape (default: the "
+                         "config's; klppo = kl_ppo_learner, a side line, not "
+                         "the headline)")
     ap.add_argument("--reference-lr", action="store_true",
                     help="raw lr on row sums as the reference (diverges at "
                          "this batch size; default: lr_scale_rows)")
@@ -231,6 +235,14 @@ def main():
               "pass --allow-kernel-override" % set_over, file=sys.stderr)
         sys.exit(2)
     cfg = select_config(args.config)
+    if args.algo:
+        global ALGO
+        ALGO = args.algo
+        if ALGO == "klppo" and not args.no_cpu_baseline:
+            print("bench.py: no CPU baseline for --algo klppo (the harness "
+                  "times ppo / actor-critic learners); pass --no-cpu-baseline",
+                  file=sys.stderr)
+            sys.exit(2)
     if args.rollout_steps:
         global T
         T = args.rollout_steps
@@ -354,9 +366,14 @@ def main():
     it_ideal_s = (policy_fwd_flops_per_env_step() / (roll_peak * 1e12) +
                   5 * value_fwd_flops_per_row() / (FP32_PEAK_TFLOPS * 1e12) +
                   3 * EPOCHS * policy_fwd_flops_per_env_step() / (train_peak * 1e12))
-    if args.config == 3:
+    if args.config == 3 and ALGO == "ppo":
         metric = "env-steps/sec (whole node) PPO bin-packing 64-bin"
         workload = "BASELINE config %d: " % (3 if world == 1 else 4)
+    elif ALGO != cfg["algo"]:
+        metric = "env-steps/sec (whole node) %s bin-packing %d-bin %d-D" % (
+            {"ppo": "PPO", "klppo": "KL-PPO", "ac": "actor-critic"}[ALGO], B, D)
+        workload = "side line, %s on the shape of BASELINE config %d: " % (
+            ALGO, args.config)
     else:
         metric = "env-steps/sec (whole node) %s bin-packing %d-bin %d-D" % (
             "PPO" if ALGO == "ppo" else "actor-critic", B, D)
@@ -378,6 +395,7 @@ def main():
         "config": {"workload": workload + cfg["name"] % n + (
                        "; larger-T point: T=%d" % T if args.rollout_steps
                        else ""),
+                   "learner": ALGO,
                    "envs_per_gpu": n, "bins": B, "dims": D, "T": T,
                    "epochs": EPOCHS, "parallelism": "dp%d" % world,
                    "lr_scale_rows": not args.reference_lr},

@@ -885,12 +885,17 @@ __global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) vo
 // Softmax of one env's 128 candidate-bin scores (lane holds bins lane and
 // 64 + lane: z[0], z[1]), the categorical sample (sequential
 // discrete_distribution order, the exact restatement near a boundary) or the
-// forced action, and the env transition into slot t+1 -- one wave.
+// forced action, and the env transition of slot t into slot t+1 -- one wave.
+// x: the env's minstd state (the caller loads / stores it); last: the
+// launch's last step (logits / probabilities outputs).  Out: nbv[k] = bin
+// k * 64 + lane in slot t+1, first = the next item is item_a.
 template <class S>
-__device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
-                                               const float (&z)[2]) {
+__device__ __forceinline__ void sample_step128_x(const RolloutArgs &a, int t, bool last,
+                                                 int env, const float (&z)[2],
+                                                 uint32_t &x, int (&nbv)[2][S::D],
+                                                 bool &first) {
   const int lane = threadIdx.x & 63;
-  const int N = a.b.N, t = a.t;
+  const int N = a.b.N;
   float p[2];
   float se = 0.0f;
 #pragma unroll
@@ -901,15 +906,14 @@ __device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
   se = seg_sum<64>(se);
   p[0] = p[0] / se;
   p[1] = p[1] / se;
-  if (a.logits_out) {
+  if (last && a.logits_out) {
     a.logits_out[(size_t)env * 128 + lane] = z[0];
     a.logits_out[(size_t)env * 128 + 64 + lane] = z[1];
   }
-  if (a.probs_out) {
+  if (last && a.probs_out) {
     a.probs_out[(size_t)env * 128 + lane] = p[0];
     a.probs_out[(size_t)env * 128 + 64 + lane] = p[1];
   }
-  uint32_t x = a.b.rng[env];
   int choice;
   if (a.forced) {
     choice = a.forced[(size_t)t * N + env];
@@ -959,14 +963,16 @@ __device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
     }
   }
   const int done = __shfl(choice < 64 ? neg[0] : neg[1], choice & 63, kWave);
-  const bool first = canonical(x) < a.env.p_a;
+  first = canonical(x) < a.env.p_a;
   const size_t o = (size_t)(t + 1) * N + env;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     int8_t *ob = a.b.bins + o * S::BD + (k * 64 + lane) * S::D;
 #pragma unroll
-    for (int d = 0; d < S::D; ++d)
-      ob[d] = (int8_t)(done ? kCapacity : nb[k][d]);
+    for (int d = 0; d < S::D; ++d) {
+      nbv[k][d] = done ? kCapacity : nb[k][d];
+      ob[d] = (int8_t)nbv[k][d];
+    }
   }
   if (lane == 0) {
     int8_t *oi = a.b.items + o * 4;
@@ -976,8 +982,20 @@ __device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
     a.b.action[(size_t)t * N + env] = choice;
     a.b.pold[(size_t)t * N + env] = pold;
     a.b.done[(size_t)t * N + env] = (uint8_t)done;
-    a.b.rng[env] = (t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
   }
+}
+
+// One step (slot a.t): sample_step128_x with the stream state read from and
+// written back to a.b.rng (jumped after step T-1).
+template <class S>
+__device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
+                                               const float (&z)[2]) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = a.b.rng[env];
+  int nbv[2][S::D];
+  bool first;
+  sample_step128_x<S>(a, a.t, true, env, z, x, nbv, first);
+  if (lane == 0) a.b.rng[env] = (a.t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
 }
 
 // ================================================ rollout step, 128 bins ===
@@ -1163,34 +1181,52 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
             h = lane >> 5;
   const int wpb = blockDim.x >> 6;
-  const int N = a.b.N, t = a.t;
+  const int N = a.b.N;
+  const int t_last = a.t + (a.nsteps > 1 ? a.nsteps : 1) - 1;
   for (int env = blockIdx.x * wpb + w; env < N; env += gridDim.x * wpb) {
-    float z[2];
-#pragma unroll 1
-    for (int hg = 0; hg < 2; ++hg) {
-      RowRaw<S> cur;
-      const size_t e = (size_t)t * N + env;
+    // slot t's rows of this lane: bins hg * 64 + rt * 32 + lr (the sampler's
+    // lane 32 rt + lr, slot hg), from global for slot a.t, then from the
+    // sampler's registers (this half's value and the partner half's)
+    int own[2][S::D], it[S::D];
+    {
+      const size_t e = (size_t)a.t * N + env;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const int bin = hg * 64 + rt * 32 + lr;
-        const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
-        const int8_t *ip = a.b.items + e * 4;
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) own[k][d] = a.b.bins[e * S::BD + (k * 64 + lane) * S::D + d];
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) it[d] = a.b.items[e * 4 + d];
+    }
+    uint32_t x = a.b.rng[env];
+    for (int t = a.t; t <= t_last; ++t) {
+      float z[2];
+#pragma unroll 1
+      for (int hg = 0; hg < 2; ++hg) {
+        RowRaw<S> cur;
 #pragma unroll
         for (int d = 0; d < S::D; ++d) {
-          cur.bv[rt][d] = bp[d];
-          cur.iv[rt][d] = ip[d];
+          const int v = hg ? own[1][d] : own[0][d];
+          const int o = __shfl_xor(v, 32, kWave);
+          cur.bv[0][d] = h ? o : v;
+          cur.bv[1][d] = h ? v : o;
+          cur.iv[0][d] = it[d];
+          cur.iv[1][d] = it[d];
         }
+        float zl[2];
+        wave_logits_split<S>(lds, cur, zl);
+        // lane = row of the half-group = bin hg*64 + lane
+        const float zh = (h ? zl[1] : zl[0]) + b3;
+        if (hg == 0)
+          z[0] = zh;
+        else
+          z[1] = zh;
       }
-      float zl[2];
-      wave_logits_split<S>(lds, cur, zl);
-      // lane = row of the half-group = bin hg*64 + lane
-      const float zh = (h ? zl[1] : zl[0]) + b3;
-      if (hg == 0)
-        z[0] = zh;
-      else
-        z[1] = zh;
+      bool first;
+      sample_step128_x<S>(a, t, t == t_last, env, z, x, own, first);
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) it[d] = first ? a.env.item_a[d] : a.env.item_b[d];
     }
-    sample_step128<S>(a, env, z);
+    if (lane == 0) a.b.rng[env] = (t_last == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
   }
 }
 
@@ -2429,6 +2465,7 @@ static hipError_t launch_rollout_one(const RolloutArgs &a, int H1, int H2,
         const int wgr = cu_count();                                          \
         info->name = "rollout_split128_kernel";                              \
         info->math = kMathSplitRollout;                                      \
+        multi = true;                                                        \
         hipLaunchKernelGGL(rollout_split128_kernel<S>,                       \
                            dim3(wgr < wg ? wgr : wg), dim3(64 * kRW),        \
                            RollSplitLds<S>::bytes, s, a);                    \

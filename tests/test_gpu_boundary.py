@@ -128,7 +128,8 @@ def test_overflowed_start_states_run_the_f32_kernels(ctx, monkeypatch, B, D,
     assert np.isfinite(wide["params"]).all()
 
 
-@pytest.mark.parametrize("B,D,widths", [(64, 2, (128, 128)), (32, 1, (64, 64))])
+@pytest.mark.parametrize("B,D,widths", [(64, 2, (128, 128)), (32, 1, (64, 64)),
+                                        (128, 3, (128, 128))])
 def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths):
     """T = 4 with an overflowed slot 0: slot 0 runs on the f32 rollout, slots
     1-3 in one launch of the register-stepping split kernel.  Teacher-forced
@@ -163,7 +164,8 @@ def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths):
 
     ref = run(True)
     got = run(False, forced=ref[BUF_ACTION])
-    assert got["kinfo"]["rollout_step"]["kernel"] == "rollout_split_kernel"
+    assert got["kinfo"]["rollout_step"]["kernel"] == (
+        "rollout_split128_kernel" if B == 128 else "rollout_split_kernel")
     for b in (BUF_ACTION, BUF_BINS, BUF_DONE, BUF_ITEMS, BUF_RNG):
         np.testing.assert_array_equal(got[b], ref[b], err_msg="buffer %d" % b)
     np.testing.assert_allclose(got[BUF_POLD], ref[BUF_POLD], rtol=2e-5, atol=1e-7)
