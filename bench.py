@@ -340,9 +340,11 @@ def main():
                                  if split else pmc_traffic())
     train_peak = kt["peak_tflops"]
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
-    # p_old, advantage (12 B); per workgroup one f32 gradient slab
+    # p_old, advantage (12 B); per workgroup of the train grid (the library
+    # reports it: 256 at configs 3 / 5, 512 at config 2) one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
-    alg_bytes = n * T * (B * D + 4 + 12) + 256 * policy_param_count(D, H1, H2) * 4
+    alg_bytes = (n * T * (B * D + 4 + 12) +
+                 kinfo["train_grid"] * policy_param_count(D, H1, H2) * 4)
     roofline = kernel_roofline(kt, flops_epoch, avg_ms)
     # whole-iteration HBM roofline (BASELINE metric: "fraction of the HBM
     # roofline"): compulsory bytes per env-step, SURVEY §8d -- env state

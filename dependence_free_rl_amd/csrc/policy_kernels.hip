@@ -659,16 +659,22 @@ __global__ __launch_bounds__(64 * kRollWaves64, roll_occ(kRollWaves64)) void rol
 // biases enter as the MFMA chains' C inputs.  The logits differ from rollout_wave_kernel's in the
 // last places (f32-class: tests/test_gpu_scale.py); the sampler, the env
 // step and everything after are the same code.
+// Layer 1 runs its k-steps over the D bin features only: the item (an
+// item-table entry in every slot these kernels see, RolloutArgs::wide
+// otherwise) is folded into a per-entry bias, (b1 + W1_item . item / 8) S_H,
+// as in the train kernels -- D = 2: one f32 MFMA per tile instead of two,
+// D = 3: two instead of three.
 // LDS (bytes): two W2 part images [o][permuted i] (H2 rows of 256 bytes: 64
 // KB at [128,128]), then f32 W1 [H1][F0], b1, b2 S_W S_H, w3 / (S_W S_H), b3,
-// S_H, the scale reduction.
+// S_H, the scale reduction, the two folded biases [2][H1].
 template <class S>
 struct RollSplitLds {
   static constexpr int W2 = 0;
   static constexpr int F = 2 * S::H2 * kImgRow;
   static constexpr int W1 = 0, B1 = S::H1 * S::F0, B2 = B1 + S::H1, W3 = B2 + S::H2,
-                       B3 = W3 + S::H2, SH = B3 + 1, SC = B3 + 4;
-  static constexpr size_t bytes = F + sizeof(float) * (SC + 2 * 16);
+                       B3 = W3 + S::H2, SH = B3 + 1, SC = B3 + 4, B1F = SC + 2 * 16;
+  static constexpr int S1F = (S::D + 1) / 2;  // layer-1 k-steps over the bins
+  static constexpr size_t bytes = F + sizeof(float) * (B1F + 2 * S::H1);
 };
 
 // Stage the f16-pair W2 images (columns permuted, see above) and the small
@@ -676,7 +682,7 @@ struct RollSplitLds {
 // synchronises the block).
 template <class S>
 __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
-                                                    char *lds) {
+                                                    const EnvDesc &env, char *lds) {
   using L = RollSplitLds<S>;
   float *lf = reinterpret_cast<float *>(lds + L::F);
   const PolicyLayout PL{S::F0, S::H1, S::H2};
@@ -724,6 +730,15 @@ __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
     lf[L::B1 + i] = P[PL.ob1() + i] * SH;
     lf[L::B2 + i] = P[PL.ob2() + i] * S2;
     lf[L::W3 + i] = P[PL.ow3() + i] * (1.0f / S2);
+    float ba = P[PL.ob1() + i], bb = ba;
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) {
+      const float wv = P[PL.oW1() + i * S::F0 + S::D + d];
+      ba += wv * ((float)env.item_a[d] / (float)kCapacity);
+      bb += wv * ((float)env.item_b[d] / (float)kCapacity);
+    }
+    lf[L::B1F + i] = ba * SH;
+    lf[L::B1F + S::H1 + i] = bb * SH;
   }
   if (threadIdx.x == 0) {
     lf[L::B3] = P[PL.ob3()];
@@ -733,9 +748,11 @@ __device__ __forceinline__ void stage_split_rollout(const float *__restrict__ P,
 
 // Partial logits (without b3) of the two r-tiles of `cur` (64 rows) by the
 // f16-pair layer 2: zl[rt] = the logit sum of row rt*32 + (lane & 31).
+// b1r[rt]: the folded layer-1 bias (LDS, x S_H) of r-tile rt's item.
 template <class S>
 __device__ __forceinline__ void wave_logits_split(const char *lds,
                                                   const RowRaw<S> &cur,
+                                                  const float *const (&b1r)[2],
                                                   float (&zl)[2]) {
   using L = RollSplitLds<S>;
   const float *lf = reinterpret_cast<const float *>(lds + L::F);
@@ -743,9 +760,13 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
   const char *w2i[2] = {lds + L::W2, lds + L::W2 + S::H2 * kImgRow};
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
-    float xb[S::S1];
+    // the bin features only (feature 2 s1 + h < D; the item is in the bias)
+    float xb[L::S1F];
 #pragma unroll
-    for (int s1 = 0; s1 < S::S1; ++s1) xb[s1] = row_feature<S>(cur, rt, 2 * s1 + h);
+    for (int s1 = 0; s1 < L::S1F; ++s1) {
+      const int f = 2 * s1 + h;
+      xb[s1] = f < S::D ? row_feature<S>(cur, rt, f) : 0.0f;
+    }
     // layer 2's accumulators start at b2 S_W S_H (C layout: register 4q + u
     // = feature ot*32 + 8q + 4h + u)
     f32x16s pre[S::NOT];
@@ -767,16 +788,16 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
       f32x16 t1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 bb = *reinterpret_cast<const float4 *>(lf + L::B1 + it * 32 + 8 * q + 4 * h);
+        const float4 bb = *reinterpret_cast<const float4 *>(b1r[rt] + it * 32 + 8 * q + 4 * h);
         t1[4 * q + 0] = bb.x;
         t1[4 * q + 1] = bb.y;
         t1[4 * q + 2] = bb.z;
         t1[4 * q + 3] = bb.w;
       }
 #pragma unroll
-      for (int s1 = 0; s1 < S::S1; ++s1) {
+      for (int s1 = 0; s1 < L::S1F; ++s1) {
         const int k = 2 * s1 + h;
-        const float wa = k < S::F0 ? lf[L::W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
+        const float wa = k < S::D ? lf[L::W1 + (it * 32 + lr) * S::F0 + k] : 0.0f;
         t1 = mfma32(wa, xb[s1], t1);
       }
       f16x8 bfr[2][2];
@@ -841,9 +862,11 @@ __global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) vo
                 "split rollout: B=64 [128,128] or B=32 [64,64]");
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   char *lds = reinterpret_cast<char *>(ldsf);
-  stage_split_rollout<S>(a.params, lds);
+  stage_split_rollout<S>(a.params, a.env, lds);
   __syncthreads();
-  const float b3 = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F)[RollSplitLds<S>::B3];
+  const float *lfr = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F);
+  const float b3 = lfr[RollSplitLds<S>::B3];
+  const float *b1fa = lfr + RollSplitLds<S>::B1F, *b1fb = b1fa + S::H1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int wpb = blockDim.x >> 6;
   const int ngroups = a.b.N / S::G;
@@ -855,11 +878,31 @@ __global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) vo
   for (int g = blockIdx.x * wpb + w; g < ngroups; g += gridDim.x * wpb) {
     const int e0 = g * S::G, env = e0 + eoff;
     RowRaw<S> cur;
-    fetch_rows<S>(a.b, a.t, e0, cur);
+    fetch_rows<S>(a.b, a.src_slot > 0 ? a.src_slot : a.t, e0, cur);
+    if (a.src_slot > 0) {  // slot 0 := slot src_slot: this lane's row
+      int8_t *ob = a.b.bins + (size_t)env * S::BD + bin * S::D;
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) ob[d] = (int8_t)(h ? cur.bv[1][d] : cur.bv[0][d]);
+      if (bin == 0) {
+        int8_t *oi = a.b.items + (size_t)env * 4;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          oi[d] = d < S::D ? (int8_t)(h ? cur.iv[1][d] : cur.iv[0][d]) : 0;
+      }
+    }
     uint32_t x = a.b.rng[env];
     for (int t = a.t; t <= t_last; ++t) {
+      // each r-tile's env's item -> its folded bias (item-table entries only)
+      const float *b1r[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        bool ia = true;
+#pragma unroll
+        for (int d = 0; d < S::D; ++d) ia &= cur.iv[rt][d] == a.env.item_a[d];
+        b1r[rt] = ia ? b1fa : b1fb;
+      }
       float zl[2];
-      wave_logits_split<S>(lds, cur, zl);
+      wave_logits_split<S>(lds, cur, b1r, zl);
       const float z = (h ? zl[1] : zl[0]) + b3;
       int nbv[S::D];
       bool first;
@@ -1175,11 +1218,12 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
                 "split rollout: B=128, [128,128]");
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   char *lds = reinterpret_cast<char *>(ldsf);
-  stage_split_rollout<S>(a.params, lds);
+  stage_split_rollout<S>(a.params, a.env, lds);
   __syncthreads();
-  const float b3 = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F)[RollSplitLds<S>::B3];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 31,
-            h = lane >> 5;
+  const float *lfr = reinterpret_cast<const float *>(lds + RollSplitLds<S>::F);
+  const float b3 = lfr[RollSplitLds<S>::B3];
+  const float *b1fa = lfr + RollSplitLds<S>::B1F, *b1fb = b1fa + S::H1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int wpb = blockDim.x >> 6;
   const int N = a.b.N;
   const int t_last = a.t + (a.nsteps > 1 ? a.nsteps : 1) - 1;
@@ -1189,16 +1233,30 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
     // sampler's registers (this half's value and the partner half's)
     int own[2][S::D], it[S::D];
     {
-      const size_t e = (size_t)a.t * N + env;
+      const size_t e = (size_t)(a.src_slot > 0 ? a.src_slot : a.t) * N + env;
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int d = 0; d < S::D; ++d) own[k][d] = a.b.bins[e * S::BD + (k * 64 + lane) * S::D + d];
 #pragma unroll
       for (int d = 0; d < S::D; ++d) it[d] = a.b.items[e * 4 + d];
+      if (a.src_slot > 0) {  // slot 0 := slot src_slot
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int d = 0; d < S::D; ++d)
+            a.b.bins[(size_t)env * S::BD + (k * 64 + lane) * S::D + d] = (int8_t)own[k][d];
+        if (lane == 0)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) a.b.items[(size_t)env * 4 + d] = d < S::D ? (int8_t)it[d] : 0;
+      }
     }
     uint32_t x = a.b.rng[env];
     for (int t = a.t; t <= t_last; ++t) {
+      bool ia = true;
+#pragma unroll
+      for (int d = 0; d < S::D; ++d) ia &= it[d] == a.env.item_a[d];
+      const float *b1r[2] = {ia ? b1fa : b1fb, ia ? b1fa : b1fb};
       float z[2];
 #pragma unroll 1
       for (int hg = 0; hg < 2; ++hg) {
@@ -1213,7 +1271,7 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
           cur.iv[1][d] = it[d];
         }
         float zl[2];
-        wave_logits_split<S>(lds, cur, zl);
+        wave_logits_split<S>(lds, cur, b1r, zl);
         // lane = row of the half-group = bin hg*64 + lane
         const float zh = (h ? zl[1] : zl[0]) + b3;
         if (hg == 0)
@@ -2427,6 +2485,15 @@ int policy_train_grid(int B, int D, int H1, int H2, int kl) {
   return cu_count();
 }
 
+// Whether launch_rollout_one would run a register-stepping split kernel for
+// a (which applies src_slot as it fetches).
+static bool rollout_fetch_shifts(const RolloutArgs &a, int H1, int H2) {
+  if (!rollout_split() || a.wide) return false;
+  const int B = a.env.B;
+  return (B == 64 && H1 == 128 && H2 == 128) || (B == 32 && H1 == 64 && H2 == 64) ||
+         (B == 128 && H1 == 128 && H2 == 128);
+}
+
 // One launch: slot a.t (multi = false), or slots a.t .. a.t + a.nsteps - 1
 // by the register-stepping split kernel (multi = true).
 static hipError_t launch_rollout_one(const RolloutArgs &a, int H1, int H2,
@@ -2555,6 +2622,19 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
   if (!info) info = &dummy;
   const int n = a.nsteps > 1 ? a.nsteps : 1;
   bool multi = false;
+  if (a.src_slot > 0 && !rollout_fetch_shifts(a, H1, H2)) {
+    // the one-slot kernels read slot 0 as it is: copy slot src_slot there
+    const size_t N = (size_t)a.b.N, BD = (size_t)a.env.B * a.env.D;
+    hipError_t e = hipMemcpyAsync(a.b.bins, a.b.bins + (size_t)a.src_slot * N * BD,
+                                  N * BD, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(a.b.items, a.b.items + (size_t)a.src_slot * N * 4, N * 4,
+                         hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    RolloutArgs a0 = a;
+    a0.src_slot = -1;
+    return launch_rollout_step(a0, H1, H2, grid, s, info);
+  }
   hipError_t e = launch_rollout_one(a, H1, H2, grid, s, info, multi);
   // a one-slot kernel ran slot a.t (its logits / probabilities are rewritten
   // by the later slots'); the rest in one launch if the kernel allows
@@ -2563,6 +2643,7 @@ hipError_t launch_rollout_step(const RolloutArgs &a, int H1, int H2, int grid,
     ak.t = a.t + k;
     ak.nsteps = n - k;
     ak.wide = 0;  // `wide` describes slot a.t only
+    ak.src_slot = -1;
     e = launch_rollout_one(ak, H1, H2, grid, s, info, multi);
   }
   return e;

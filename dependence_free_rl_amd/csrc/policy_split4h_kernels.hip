@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   S4H_STAMP(a, kKG, w, l, 1);
 
   for (int j = 0; j < J; ++j) {
-    const int gj = j < kKG ? j : kTraceGroups;  // stamped groups
+    [[maybe_unused]] const int gj = j < kKG ? j : kTraceGroups;  // stamped groups
     S4H_STAMP(a, gj, w, l, 0);
     const int cs = j % 3, ns = (j + 2) % 3;  // slots of groups j and j + 2
     int rdb = rdb0, trm0 = trm00, trm1 = trm10, stb = stb0;

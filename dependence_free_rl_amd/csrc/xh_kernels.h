@@ -68,8 +68,14 @@ struct RolloutArgs {
   float *logits_out;      // optional [N][B] (debug / parity)
   float *probs_out;       // optional [N][B]
   float *qold_out;        // KL-PPO: [T][N][B] the sampled distribution
-  int wide;  // slot t holds a bin below -capacity: the f32-MFMA kernels run
-             // (the f16-pair ones bound |bins / capacity| by 1)
+  int wide;  // slot t holds a bin below -capacity (the f16-pair rollouts
+             // bound |bins / capacity| by 1) or an item outside the item
+             // table (they fold the item into per-entry biases): the f32
+             // kernels run that slot
+  int src_slot;  // > 0 (with t == 0): slot 0 := slot src_slot first
+                 // (replay_buffer::forget keeping the open trajectories), done
+                 // by the register-stepping kernels as they fetch, else by
+                 // copies before the launch; 0 / -1: slot 0 as it is
   int nsteps;  // slots t .. t + nsteps - 1 (0 = 1); logits_out / probs_out
                // receive the last one's.  launch_rollout_step runs them in
                // one launch where the kernel steps in registers

@@ -573,17 +573,26 @@ int do_rollout(xh_trainer *t) {
     t->items_ok[0] = 1;
   }
   if (t->bins_wide.size() != T + 1) t->bins_wide.assign(T + 1, 0);
-  if (t->need_shift) {  // replay_buffer::forget(): open trajectories continue
-    HIPCHK(hipMemcpyAsync(t->bins, t->bins + T * N * t->BD(), N * t->BD(),
-                          hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(t->items, t->items + T * N * 4, N * 4,
-                          hipMemcpyDeviceToDevice, s));
+  // replay_buffer::forget(): open trajectories continue from slot T.  With
+  // no host overrides pending the rollout launch moves slot T to slot 0
+  // itself (the register-stepping kernels as they fetch; copies otherwise)
+  int src_slot = -1;
+  if (t->need_shift) {
+    if (t->env_override.empty()) {
+      src_slot = (int)T;
+    } else {
+      HIPCHK(hipMemcpyAsync(t->bins, t->bins + T * N * t->BD(), N * t->BD(),
+                            hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemcpyAsync(t->items, t->items + T * N * 4, N * 4,
+                            hipMemcpyDeviceToDevice, s));
+    }
     t->need_shift = false;
     t->items_ok[0] = t->items_ok[T];
     t->bins_wide[0] = t->bins_wide[T];
   }
   CHK(apply_env_overrides(t));  // whole item-table entries only
   xh::RolloutArgs a{};
+  a.src_slot = src_slot;
   a.env = t->env;
   a.b = t->batch();
   a.jump_mul = t->jump_mul;
@@ -594,7 +603,10 @@ int do_rollout(xh_trainer *t) {
   // only slot 0 can hold a wide state
   a.t = 0;
   a.nsteps = (int)T;
-  a.wide = t->bins_wide[0];
+  // the f32 kernels for a slot 0 the split rollouts cannot take: a bin below
+  // -capacity, or an item outside the item table (set_buffer; the split
+  // rollouts fold the item into per-entry biases)
+  a.wide = t->bins_wide[0] || !t->items_ok[0];
   a.logits_out = t->logits;
   a.probs_out = t->probs;
   CHK(timed(t, "rollout_step", [&]() {

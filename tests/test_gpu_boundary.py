@@ -128,12 +128,15 @@ def test_overflowed_start_states_run_the_f32_kernels(ctx, monkeypatch, B, D,
     assert np.isfinite(wide["params"]).all()
 
 
+@pytest.mark.parametrize("kind", ["bin", "item"])
 @pytest.mark.parametrize("B,D,widths", [(64, 2, (128, 128)), (32, 1, (64, 64)),
                                         (128, 3, (128, 128))])
-def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths):
-    """T = 4 with an overflowed slot 0: slot 0 runs on the f32 rollout, slots
-    1-3 in one launch of the register-stepping split kernel.  Teacher-forced
-    with the all-f32 run's actions, every state, item, done and RNG state is
+def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths, kind):
+    """T = 4 with a slot 0 the split rollouts cannot take -- an overflowed
+    bin, or an item outside the item table (they fold the item into
+    per-entry biases): slot 0 runs on the f32 rollout, slots 1-3 in one
+    launch of the register-stepping split kernel.  Teacher-forced with the
+    all-f32 run's actions, every state, item, done and RNG state is
     bit-identical to that run, and p_old agrees to f32 rounding."""
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
@@ -150,9 +153,14 @@ def test_wide_slot0_then_register_stepping(ctx, monkeypatch, B, D, widths):
                      widths=widths, rng_state=91)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
-        bins, items = tr.env_state()
-        bins[5, 3, 0] = -40
-        tr.set_env_state(0, bins, items)
+        if kind == "bin":
+            bins, items = tr.env_state()
+            bins[5, 3, 0] = -40
+            tr.set_env_state(0, bins, items)
+        else:
+            it = tr.buffer(BUF_ITEMS).copy()
+            it[0, 5, :D] = 3  # not an item-table entry
+            tr.set_buffer(BUF_ITEMS, it)
         if forced is not None:
             tr.set_forced_actions(forced)
         tr.rollout()
