@@ -66,7 +66,7 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 # unless --allow-kernel-override is given):
 KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL", "XH_VALUE_KERNEL")
 HBM_PEAK_GBS = 8000.0
-PHASE_ITERS = 2  # the phase-breakdown pass after the timed region
+PHASE_ITERS = 3  # the phase-breakdown pass after the timed region
 
 
 def kernel_roofline(k, flops_per_launch, avg_ms):
@@ -312,6 +312,7 @@ def main():
     # the phase breakdown: PHASE_ITERS more iterations (every rank), every
     # launch timed
     tr.set_timing(True)
+    tr.iterate(1)  # (the events' own first use)
     tr.reset_timing()
     tr.iterate(PHASE_ITERS)
     tr.synchronize()
