@@ -415,17 +415,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     }
   };
   // partial logits of rows 16 rt + li over this wave's features -> F_Z[zs]
-  auto partial = [&](const f32x4 &pre, const f32x4 &w3, int zs, int rt) {
-    float zp = relu(pre[0]) * w3[0];
-    zp = fmaf(relu(pre[1]), w3[1], zp);
-    zp = fmaf(relu(pre[2]), w3[2], zp);
-    zp = fmaf(relu(pre[3]), w3[3], zp);
-    zp = sum_groups(zp);
-    if (G == 0) lf[F_Z + zs * 256 + (16 * rt + li) * kNW + w] = zp;
-  };
   auto partials = [&](const f32x4 (&pre)[4], const f32x4 &w3, int zs) {
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) partial(pre[rt], w3, zs, rt);
+    for (int rt = 0; rt < 4; ++rt) {
+      float zp = relu(pre[rt][0]) * w3[0];
+      zp = fmaf(relu(pre[rt][1]), w3[1], zp);
+      zp = fmaf(relu(pre[rt][2]), w3[2], zp);
+      zp = fmaf(relu(pre[rt][3]), w3[3], zp);
+      zp = sum_groups(zp);
+      if (G == 0) lf[F_Z + zs * 256 + (16 * rt + li) * kNW + w] = zp;
+    }
   };
   auto no_task = [](int) {};
 
@@ -469,8 +468,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     bool iaA = false, iaB = false;
     float b1tA = 0.0f, b1tB = 0.0f;
     f32x4 w3;
-    f32x4 pre_nx[4];
-    const int zs = (j + 1) & 1;
     auto xtask = [&](int k) {
       if (k == 0) {
         ex = __expf(((z4[0] + z4[1]) + (z4[2] + z4[3])) + b3);
@@ -519,7 +516,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h) gx0[h] = lds4v(xim + 16 * h + 4 * G);
       } else if (k == 4) {
-        w3 = lds4v(lf + F_W3 + fo);  // for the partial logits of group j+1
         gr4 = lds4v(gp + 4 * li);  // g of rows 16 rt + li
 #pragma unroll
         for (int h = 0; h < 2; ++h) ggk[h] = lds4v(gw + 16 * h + 4 * G);
@@ -559,19 +555,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
           bq0[1][4 * h + jj] = p1;
           bq0[2][4 * h + jj] = p2;
         }
-      } else if (k == 16 || k == 19 || k == 23) {
-        // group j+1's partial logits of r-tile 0 / 1 / 2, whose layer-2
-        // accumulation ended one K-step slot earlier (r-tile 3's after the
-        // loop)
-        const int rt = k == 16 ? 0 : (k == 19 ? 1 : 2);
-        partial(pre_nx[rt], w3, zs, rt);
+      } else if (k == 20) {
+        w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 22) {
         if (w == 0) stage_store(raw, ns);  // group j+2's rows
       }
     };
+    f32x4 pre_nx[4];
     layer2(rdb, pre_nx, xtask);
     S4H_STAMP(a, gj, w, l, 1);
-    partial(pre_nx[3], w3, zs, 3);
+    partials(pre_nx, w3, (j + 1) & 1);
     S4H_STAMP(a, gj, w, l, 2);
     __syncthreads();
     S4H_STAMP(a, gj, w, l, 3);
