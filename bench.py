@@ -339,6 +339,10 @@ def main():
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
     traffic, traffic_src, pmc = (pmc_traffic(kt["kernel"], any_shape=True)
                                  if split else pmc_traffic())
+    if args.rollout_steps and args.rollout_steps != cfg["T"]:
+        # the PMC passes profile the config's own T: their bytes per launch
+        # are not this launch's
+        traffic, traffic_src = None, None
     train_peak = kt["peak_tflops"]
     # compulsory bytes of one epoch: per env-step state (B*D + 4 B) + action,
     # p_old, advantage (12 B); per workgroup of the train grid (the library
