@@ -105,7 +105,8 @@ __global__ __launch_bounds__(kELB) void end_write_kernel(EndListArgs a,
       if (a.done[(size_t)t * a.N + e]) a.end_list[pos++] = t * a.N + e;
 }
 
-// The same list in one launch of one workgroup for N <= 1024 C, N % 4 == 0:
+// The same list in one launch of one workgroup for N <= 1024 C, N % 4 == 0
+// (used up to C = 8):
 // thread i owns envs [i C, (i+1) C), reads their done bytes as 32-bit words
 // (independent loads), keeps one count per env in registers, one block-wide
 // exclusive scan of the thread totals, then writes its envs' entries (t outer,
@@ -183,15 +184,14 @@ int end_list_scratch_ints(int N) { return 2 * ((N + kELB - 1) / kELB); }
 
 hipError_t launch_end_list(const EndListArgs &a, int *scratch,
                                hipStream_t s) {
-  if (a.N % 4 == 0 && a.N <= 1024 * 32) {
+  // one workgroup up to 8192 envs (config 2: 6 us against 14 us + two
+  // launch gaps); the parallel three passes beyond (measured at 32768 envs:
+  // 36 us in one workgroup, 14 us in three passes)
+  if (a.N % 4 == 0 && a.N <= 1024 * 8) {
     if (a.N <= 1024 * 4)
       hipLaunchKernelGGL(end_list_kernel<4>, dim3(1), dim3(1024), 0, s, a);
-    else if (a.N <= 1024 * 8)
-      hipLaunchKernelGGL(end_list_kernel<8>, dim3(1), dim3(1024), 0, s, a);
-    else if (a.N <= 1024 * 16)
-      hipLaunchKernelGGL(end_list_kernel<16>, dim3(1), dim3(1024), 0, s, a);
     else
-      hipLaunchKernelGGL(end_list_kernel<32>, dim3(1), dim3(1024), 0, s, a);
+      hipLaunchKernelGGL(end_list_kernel<8>, dim3(1), dim3(1024), 0, s, a);
     return hipGetLastError();
   }
   const int nblk = (a.N + kELB - 1) / kELB;
