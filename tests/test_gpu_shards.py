@@ -23,6 +23,10 @@ pytestmark = pytest.mark.gpu
 # values (r03: 2.9e-4 relative L2; r04: 4.9e-4 / 1.4e-3,
 # profiles/r04*_shard_sums.jsonl)
 SHARD_SUM_LIMITS_B64 = (1.5e-3, 4e-3)
+# B = 128, 3-D, n = 8192 (config 5's shape on its own kernels; the
+# oracle-pinned check of the same kernels is the n = 48 case): about 3x the
+# measured (r04: 1.2e-3 / 2.7e-3 and 1.9e-3 / 8.0e-3 over the two iterations)
+SHARD_SUM_LIMITS_B128 = (6e-3, 2.5e-2)
 
 
 def _log_shard_sum(B, n, it, rel, worst):
@@ -44,6 +48,9 @@ def _log_shard_sum(B, n, it, rel, worst):
     # a config-4 rank's situation (env_offset != 0, num_envs_global > N)
     (64, 2, (128, 128), 128),     # oracle-pinned, several groups per workgroup
     (64, 2, (128, 128), 16384),   # config 3 = two config-4 ranks' shards
+    # config 5's shape (128 bins, 3-D) on its own kernels
+    (128, 3, (128, 128), 48),     # oracle-pinned, several units per workgroup
+    (128, 3, (128, 128), 8192),   # config 5 = two ranks' shards
 ])
 def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
@@ -63,13 +70,15 @@ def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
         return tr
 
     full, s0, s1 = make(2 * n, 0), make(n, 0), make(n, n)
-    if B == 64:  # the headline kernels ran, on every trainer
+    if B >= 64:  # the f16-pair kernels ran, on every trainer
+        want = ((HEADLINE_TRAIN_KERNEL, "rollout_split_kernel") if B == 64 else
+                ("policy_train_split8x_kernel", "rollout_split128_kernel"))
         for tr in (full, s0, s1):
             tr.rollout()
             tr.learn()
             k = tr.kernel_info()
-            assert k["policy_train"]["kernel"] == HEADLINE_TRAIN_KERNEL, k
-            assert k["rollout_step"]["kernel"] == "rollout_split_kernel", k
+            assert k["policy_train"]["kernel"] == want[0], k
+            assert k["rollout_step"]["kernel"] == want[1], k
         full, s0, s1 = make(2 * n, 0), make(n, 0), make(n, n)
     orc = None
     if n <= 128:  # the oracle's sum|terms| per entry states the fp32 bound
@@ -121,7 +130,8 @@ def test_two_shards_sum_to_full_batch(ctx, B, D, widths, n):
             # bins; the measured pair is logged per run)
             rel = np.linalg.norm(g - f) / np.linalg.norm(f)
             worst = np.abs(g - f).max() / np.abs(f).max()
-            lim = (1e-5, 1e-4) if B == 8 else SHARD_SUM_LIMITS_B64
+            lim = (1e-5, 1e-4) if B == 8 else (
+                SHARD_SUM_LIMITS_B64 if B == 64 else SHARD_SUM_LIMITS_B128)
             _log_shard_sum(B, n, it, rel, worst)
             assert rel <= lim[0] and worst <= lim[1], (rel, worst)
 
