@@ -157,16 +157,6 @@ __device__ __forceinline__ int relu_bit(float x) {
   asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m) : "v"(__float_as_int(x)));
   return m;
 }
-// sum over the four lane groups (rows of 16 lanes) without an LDS round
-// trip: ((g0 + g1) + (g2 + g3)) in every lane, as two __shfl_xor steps
-__device__ __forceinline__ float sum_groups(float v) {
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
-                                                  false, false);
-  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
-                                                  false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
 __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
@@ -415,16 +405,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     }
   };
   // partial logits of rows 16 rt + li over this wave's features -> F_Z[zs]
+  // (lane group G ends with r-tile G's sum: sum_groups_t)
   auto partials = [&](const f32x4 (&pre)[4], const f32x4 &w3, int zs) {
+    float zp[4];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) {
-      float zp = relu(pre[rt][0]) * w3[0];
-      zp = fmaf(relu(pre[rt][1]), w3[1], zp);
-      zp = fmaf(relu(pre[rt][2]), w3[2], zp);
-      zp = fmaf(relu(pre[rt][3]), w3[3], zp);
-      zp = sum_groups(zp);
-      if (G == 0) lf[F_Z + zs * 256 + (16 * rt + li) * kNW + w] = zp;
+      zp[rt] = relu(pre[rt][0]) * w3[0];
+      zp[rt] = fmaf(relu(pre[rt][1]), w3[1], zp[rt]);
+      zp[rt] = fmaf(relu(pre[rt][2]), w3[2], zp[rt]);
+      zp[rt] = fmaf(relu(pre[rt][3]), w3[3], zp[rt]);
     }
+    lf[F_Z + zs * 256 + (16 * G + li) * kNW + w] = sum_groups_t(zp);
   };
   auto no_task = [](int) {};
 

@@ -91,6 +91,29 @@ __device__ __forceinline__ float half_swap(float v) {
   return __uint_as_float((threadIdx.x & 32) ? a : b);
 }
 
+// The sums over the four lane groups (rows of 16 lanes) of four values at
+// once, for the MFMA C layout's partial dot products (config 2's train
+// kernel, policy_split4h_kernels.hip: 0.0700 -> 0.0686 ms per epoch; the
+// 8-wave kernels measured slower with it and keep one swap pair per value):
+// lane group G returns (v[G] of group 0 + group 1) + (groups 2 + 3) -- the
+// bits of two self-swap steps (permlane16 then permlane32) per value, in three
+// swaps and three adds instead of eight of each plus the copy each self-swap
+// needs.
+// v_permlane16_swap exchanges the first operand's odd rows with the second's
+// even rows, so after (v0, v1) row 2k holds v0 and row 2k+1 v1, summed over
+// rows 2k and 2k+1; v_permlane32_swap (the first operand's upper half with the
+// second's lower half) then pairs the two halves.
+__device__ __forceinline__ float sum_groups_t(const float (&v)[4]) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                  false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[2]), __float_as_uint(v[3]),
+                                                  false, false);
+  const float s01 = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const float s23 = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(s01), __float_as_uint(s23),
+                                                  false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
 // v + (v of a partner lane) through a DPP lane pattern (a VALU modifier, no
 // LDS round trip).
 template <int CTRL>
