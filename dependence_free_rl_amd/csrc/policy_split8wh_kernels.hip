@@ -69,6 +69,21 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Built twice (Makefile): the PPO / actor-critic kernel (the benchmark's),
+// and with XH_8WH_KL_TU=1 (policy_split8wh_kl_kernels.o) its KL-PPO form,
+// policy_train_split8wh_kl_kernel.  The KL additions are preprocessor blocks
+// so that the PPO object compiles from exactly its measured source (the
+// kernel's register allocation moves with any change to it), and the KL
+// object gets the higher full-unroll threshold its larger task lambdas need.
+#ifndef XH_8WH_KL_TU
+#define XH_8WH_KL_TU 0
+#endif
+#if XH_8WH_KL_TU
+#define KLTU(...) __VA_ARGS__
+#else
+#define KLTU(...)
+#endif
+
 // Phase stamps (trace build, tools/build_trace8wp.sh: -DXH_DIAG_TRACE=1, run
 // with XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
 // workgroups records the cycle counter at 0 X start, 1 layer 2 (+ group j's
@@ -138,7 +153,12 @@ constexpr int F_XP = F_X + 3 * kD * 64;  // [3 slots][2 dims][16 li][4 rt]
 constexpr int F_IT = F_XP + 3 * kD * 64;  // [3 slots] the group's item is item_a
 constexpr int F_REC = F_IT + 4;        // [3 slots][action bits, pold, adv, -]
 constexpr int F_SC = F_REC + 3 * 4;    // [16]: scale reduction scratch, the scales
+#if XH_8WH_KL_TU
+constexpr int F_Q = F_SC + 16;         // KL-PPO: [3 slots][64 bins] old distribution
+constexpr int F_END = F_Q + 3 * 64;
+#else
 constexpr int F_END = F_SC + 16;
+#endif
 constexpr size_t kLds = L_F + sizeof(float) * F_END;
 static_assert(kLds <= 160 * 1024, "LDS");
 static_assert(F_REC % 4 == 0 && F_GW % 4 == 0 && F_GP % 4 == 0 && F_X % 4 == 0 && F_XP % 4 == 0 &&
@@ -250,8 +270,21 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
+#if XH_8WH_KL_TU
+// kl_ppo_learner's epoch (policy_gradient.h:310-335) over every row of its
+// state matrix, as policy_train_kernel<S, true> (policy_kernels.hip): the T N
+// transitions, then the open trajectories' end rows (slot T, q of step T - 1,
+// valid unless step T - 1 ended), then the terminal end rows E_t of end_list
+// (bins with the item taken back out of the chosen bin, rl.h:336-343); end
+// rows have A = 0.  The loss head is kl_regulated_loss through
+// softmax_layer::backward, and each workgroup sums KL(q || p) over its valid
+// rows into kl_part.
+__global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kl_kernel(
+    PolicyTrainArgs a) {
+#else
 __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     PolicyTrainArgs a) {
+#endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
   const PolicyLayout PL{kF0, kH, kH};
@@ -259,7 +292,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int l = tid & 63, G = l >> 4, li = l & 15;
+#if XH_8WH_KL_TU
+  const int NT = a.b.T * a.b.N;
+  const int n_end = *a.n_end;
+  const int ngroups = NT + a.b.N + n_end;
+  const float beta = *a.beta;
+#else
   const int ngroups = a.b.T * a.b.N;
+#endif
   // this workgroup's groups: g_j = blockIdx.x + j gridDim.x, j < J; indices
   // past the end are clamped to the last group (their work is discarded)
   const int J = (int)blockIdx.x < ngroups
@@ -382,6 +422,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     for (int j = 0; j < 4; ++j) accW2[ot][j] = 0.0f;
   float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float accB3 = 0.0f, w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
+#if XH_8WH_KL_TU
+  double kl_acc = 0.0;  // sum of KL(q || p) over this wave's rows
+#endif
 
   // wave 0 stages group j+2 during X(j): raw loads at its start (two
   // registers: the row's bins; lanes 0-3 the action, old probability,
@@ -389,11 +432,44 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   // (bins / 8 in row order and in the C layout's order, whether the item is
   // item_a, the record) late in the same phase, so the loads' latency hides
   // under layer 2
+#if XH_8WH_KL_TU
+  struct Raw {
+    int bi, rec;
+    float q;     // the old distribution's entry of bin l
+    int ended;   // open end rows: step T - 1 of the env ended
+  };
+  // the row of the [T+1][N] arrays group g reads and the row of its old
+  // distribution (kind 0 transition, 1 open end row, 2 terminal end row); g
+  // is wave-uniform: scalar branches, and only terminal end rows wait for
+  // their end_list entry
+  auto kl_rows = [&](int g, size_t &ti, size_t &qi) {
+    const int N = a.b.N;
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g < NT) {
+      ti = qi = (size_t)g;
+    } else if (g < NT + N) {
+      ti = (size_t)NT + (g - NT);
+      qi = (size_t)(NT - N) + (g - NT);
+    } else {
+      const int jj = min(g - NT - N, max(n_end - 1, 0));
+      const int te = __builtin_amdgcn_readfirstlane(a.end_list[jj]);
+      ti = qi = (size_t)te;
+    }
+  };
+  auto stage_load = [&](int j) {
+    size_t ti = tindex(j), qi = 0;
+    kl_rows((int)ti, ti, qi);
+    // (open end rows: the [T][N] record arrays end at slot T - 1; their
+    // values are not used for end rows)
+    const size_t ri = qi;
+#else
   struct Raw {
     int bi, rec;
   };
   auto stage_load = [&](int j) {
     const size_t ti = tindex(j);
+    const size_t ri = ti;
+#endif
     int lo = l * kD;  // recomputed per use rather than held (register pressure)
     asm volatile("" : "+v"(lo));
     const int bins =
@@ -401,18 +477,37 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     // one branch-free load per lane (lanes 3.. the item's first two
     // coordinates), so nothing waits for it before its use
     // (the address chosen by selects, not branches)
-    const unsigned long long p0 = (unsigned long long)(a.b.action + ti);
-    const unsigned long long p1 = (unsigned long long)(a.b.pold + ti);
-    const unsigned long long p2 = (unsigned long long)(a.adv + ti);
+    const unsigned long long p0 = (unsigned long long)(a.b.action + ri);
+    const unsigned long long p1 = (unsigned long long)(a.b.pold + ri);
+    const unsigned long long p2 = (unsigned long long)(a.adv + ri);
     const unsigned long long p3 = (unsigned long long)(a.b.items + ti * 4);
     unsigned long long pa = l >= 3 ? p3 : p2;
     pa = l == 1 ? p1 : pa;
     pa = l == 0 ? p0 : pa;
+#if XH_8WH_KL_TU
+    Raw r{bins, *reinterpret_cast<const int *>(pa), a.qold[qi * kB + l], 0};
+    const int g = __builtin_amdgcn_readfirstlane((int)tindex(j));
+    if (g >= NT && g < NT + a.b.N) r.ended = a.b.done[qi];
+    return r;
+  };
+  auto stage_store = [&](const Raw &r, int s, int j) {
+    const int g = __builtin_amdgcn_readfirstlane((int)tindex(j));
+    const int kind = g < NT ? 0 : g < NT + a.b.N ? 1 : 2;
+    // the terminal view: the chosen bin without the item (rl.h:336-343)
+    const int itm = __builtin_amdgcn_readlane(r.rec, 3);
+    const bool sub = kind == 2 && l == __builtin_amdgcn_readfirstlane(r.rec);
+    const int b0 = (signed char)(r.bi & 0xff) - (sub ? (signed char)(itm & 0xff) : 0);
+    const int b1 = (signed char)((r.bi >> 8) & 0xff) - (sub ? (signed char)((itm >> 8) & 0xff) : 0);
+    const float x0 = (float)b0 / (float)kCapacity;
+    const float x1 = (float)b1 / (float)kCapacity;
+    lf[F_Q + s * 64 + l] = r.q;
+#else
     return Raw{bins, *reinterpret_cast<const int *>(pa)};
   };
   auto stage_store = [&](const Raw &r, int s) {
     const float x0 = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
     const float x1 = (float)(signed char)((r.bi >> 8) & 0xff) / (float)kCapacity;
+#endif
     const int pl = 4 * (l & 15) + (l >> 4);
     lf[F_X + s * 128 + l] = x0;
     lf[F_X + s * 128 + 64 + l] = x1;
@@ -422,7 +517,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     const int i0 = (signed char)(item & 0xff), i1 = (signed char)((item >> 8) & 0xff);
     if (l == 0)
       lf[F_IT + s] = (i0 == a.env.item_a[0] && i1 == a.env.item_a[1]) ? 1.0f : 0.0f;
+#if XH_8WH_KL_TU
+    // the record: action (lane 0), advantage (lane 2, 0 for end rows), whether
+    // the row counts (lane 3: not a terminal row past n_end, nor an open end
+    // row whose env ended at step T - 1)
+    const int ended = __builtin_amdgcn_readfirstlane(r.ended);
+    const bool valid = kind == 0 || (kind == 1 ? ended == 0 : g - NT - a.b.N < n_end);
+    if (l == 0 || l == 2) lf[F_REC + 4 * s + l] = kind == 0 ? __int_as_float(r.rec) : 0.0f;
+    if (l == 3) lf[F_REC + 4 * s + 3] = valid ? 1.0f : 0.0f;
+#else
     if (l < 3) lf[F_REC + 4 * s + l] = __int_as_float(r.rec);
+#endif
   };
   // H1 values (C layout, r-tile rt) scaled by S_H -> the two f16 part images
   auto store_h1 = [&](const f32x4 &t, int sb, int rt) {
@@ -508,8 +613,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   // layer 1 and layer 2 of group 0 (its partial logits), layer 1 of group 1
   f32x4 pre_cur[4];
   if (w == 0) {
-    stage_store(stage_load(0), 0);
-    stage_store(stage_load(1), 1);
+    stage_store(stage_load(0), 0 KLTU(, 0));
+    stage_store(stage_load(1), 1 KLTU(, 1));
   }
   __syncthreads();
   layer1_all(0, stb0);
@@ -541,6 +646,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     const float b3 = lf[F_B3];
     const f32x4 rec = lds4v(lf + F_REC + 4 * cs);
     const float itc = lf[F_IT + cs];
+#if XH_8WH_KL_TU
+    const float qv = lf[F_Q + cs * 64 + l];
+    float kp = 0.0f, kg = 0.0f;
+#endif
     f32x4 gx0[2], gx1[2];
     float ex = 0.0f, se = 0.0f, gz = 0.0f;
     f32x4 gr4, ggk[2], hT[2];
@@ -559,6 +668,22 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
         ex = __expf(zs + b3);
       } else if (k == 1) {
         se = seg_sum<64>(ex);
+#if XH_8WH_KL_TU
+      } else if (k == 2) {
+        // kl_regulated_loss (policy_gradient.h:41-85): softmax_gradient_log
+        // + beta (p - q) as a probability-space gradient, through
+        // softmax_layer::backward (nn.h:393-417) in the next slot; the KL sum
+        // on one wave per group, in turn
+        const int cu = __builtin_amdgcn_readfirstlane(__float_as_int(rec[0]));
+        const float Ac = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rec[2])));
+        const float p = ex * __builtin_amdgcn_rcpf(se);
+        float gpv = fmaf(beta, p - qv, p * Ac);
+        if (l == cu) gpv -= Ac;
+        kp = p;
+        kg = gpv;
+        const bool vld = __builtin_amdgcn_readfirstlane(__float_as_int(rec[3])) != 0;
+        if (vld && (j & 7) == w) kl_acc += (double)(qv * logf(qv / p));
+#else
       } else if (k == 2) {
         const int cu = __builtin_amdgcn_readfirstlane(__float_as_int(rec[0]));
         const float po = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rec[1])));
@@ -580,7 +705,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
           gz = p * Ac;
           if (l == cu) gz -= Ac;
         }
+#endif
       } else if (k == 3) {
+#if XH_8WH_KL_TU
+        {
+          const float sgv = seg_sum<64>(kp * kg);
+          const bool vld = __builtin_amdgcn_readfirstlane(__float_as_int(rec[3])) != 0;
+          gz = vld ? kp * (kg - sgv) : 0.0f;
+        }
+#endif
         gw[l] = gz;
         gp[4 * (l & 15) + (l >> 4)] = gz;
         accB3 += gz;  // wave 0's is written out
@@ -661,7 +794,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 44) {
         // wave 0: group j+2's rows (loaded at the start of X(j)) into slot ns
-        if (w == 0) stage_store(raw, ns);
+        if (w == 0) stage_store(raw, ns KLTU(, j + 2));
       }
     };
     f32x4 pre_nx[4];
@@ -823,6 +956,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     for (int rt = 0; rt < 4; ++rt) pre_cur[rt] = pre_nx[rt];
   }
 
+#if XH_8WH_KL_TU
+  {
+    // the workgroup's KL sum (the loop's last barrier is behind: F_Z is free)
+    double v = kl_acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+    double *kd = reinterpret_cast<double *>(lf + F_Z);
+    if (l == 0) kd[w] = v;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int v8 = 0; v8 < 8; ++v8) t += kd[v8];
+      a.kl_part[blockIdx.x] = t;
+    }
+  }
+#endif
+
   // ---------------------------------------------------- slab write-out ----
   // every entry has exactly one producing lane
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
@@ -881,8 +1032,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
 
 }  // namespace s8h
 
+#if XH_8WH_KL_TU
+hipError_t launch_policy_train_split8wh_kl(const PolicyTrainArgs &a, int grid,
+                                           hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)s8h::policy_train_split8wh_kl_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s8h::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(s8h::policy_train_split8wh_kl_kernel, dim3(grid),
+                     dim3(s8h::kThreads), s8h::kLds, s, a);
+  return hipGetLastError();
+}
+#else
 hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s) {
+  if (a.algo == kKLPPO) return launch_policy_train_split8wh_kl(a, grid, s);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)s8h::policy_train_split8wh_kernel,
@@ -894,5 +1061,6 @@ hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                      dim3(s8h::kThreads), s8h::kLds, s, a);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace xh

@@ -3,10 +3,11 @@
 // Product kernels (libxylo_hip.so), f16 pairs + the exact bf16 split
 // (DESIGN.md §3.0a-d):
 //   64 bins, 2-D, [128,128] (configs 3 / 4)  policy_train_split8wh_kernel
+//                                  (KL-PPO: policy_train_split8wh_kl_kernel)
 //   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
 //   32 bins, 1-D, [64,64] (config 2)         policy_train_split4h_kernel
-// and the f32-MFMA kernels of policy_kernels.hip for every other shape, for
-// KL-PPO, and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
+// and the f32-MFMA kernels of policy_kernels.hip for every other shape (KL-PPO
+// included), and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
 // kernels' tests).
 //
 // The superseded config-3 / config-5 forms (split4w, split8w, split8wp,
@@ -49,6 +50,9 @@ static bool train_kernel_is(const char *name) {
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
   const bool algo = a.algo == kPPO || a.algo == kAC;
+  // KL-PPO: the 64-bin 2-D kernel only (its KL instantiation)
+  if (a.algo == kKLPPO)
+    return H1 == 128 && H2 == 128 && a.env.B == 64 && a.env.D == 2;
   if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
     return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
   return algo && H1 == 128 && H2 == 128 &&
@@ -79,7 +83,8 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
 #endif
   } else {
     if (!ov) {
-      info->name = "policy_train_split8wh_kernel";
+      info->name = a.algo == kKLPPO ? "policy_train_split8wh_kl_kernel"
+                                    : "policy_train_split8wh_kernel";
       return launch_policy_train_split8wh(a, grid, s);
     }
 #if XH_VARIANT_KERNELS

@@ -373,6 +373,10 @@ hipError_t launch_policy_train_split4p(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8wh(const PolicyTrainArgs &a, int grid,
                                         hipStream_t s);
+// its KL-PPO build (policy_split8wh_kl_kernels.o; called by
+// launch_policy_train_split8wh)
+hipError_t launch_policy_train_split8wh_kl(const PolicyTrainArgs &a, int grid,
+                                           hipStream_t s);
 hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,

@@ -1,0 +1,83 @@
+"""KL-PPO on the 64-bin f16-pair train kernel, against the oracle.
+
+kl_ppo_learner (/root/reference/xylo/policy_gradient.h:310-335) trains on
+every row of its state matrix: the transitions, the open trajectories' end
+rows and the terminal end rows (rl.h:336-343), with kl_regulated_loss
+(policy_gradient.h:41-85) and beta adapted between epochs from the mean KL.
+At the 64-bin 2-D [128,128] shape (BASELINE config 3's) the epoch runs
+policy_train_split8wh_kl_kernel, the KL-PPO build of the headline train
+kernel (f16 pairs + the exact bf16 split).  Lockstep iterations: the oracle learns from the
+device trainer's parameters each iteration, samples its own actions and the
+device replays them, so the comparison measures one learn()'s arithmetic.
+Several iterations carry the envs into terminal end rows (a 64-bin episode
+ends when an item overflows its bin).  Epoch-0 gradients are held to the
+tight budget (conftest), later epochs to the drift budget; beta (used and
+after) must equal the oracle's, the mean KL within 1e-4.
+"""
+import numpy as np
+import pytest
+
+from conftest import GRAD_UNITS_P99_DRIFT, assert_close, assert_grad_units
+from gpu_helpers import step_major
+
+pytestmark = pytest.mark.gpu
+
+KL_KERNEL = "policy_train_split8wh_kl_kernel"
+
+
+@pytest.mark.parametrize("N,T,iters,cap,kernel",
+                         [(48, 4, 5, 0, "split"), (32, 4, 4, 1, "split"),
+                          (48, 4, 5, 0, "f32")],
+                         ids=["n48", "n32_cap1", "n48_f32"])
+def test_klppo_split_matches_oracle(ctx, monkeypatch, N, T, iters, cap, kernel):
+    """kernel "f32": the same iterations on the f32-MFMA KL kernel
+    (XH_TRAIN_KERNEL=f32), the accuracy reference the split kernel's logged
+    error units are read against."""
+    from oracle import pyoracle as po
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import BUF_KL, BUF_POLICY_GRADS
+    B, D, widths, x0, wd = 64, 2, (128, 128), 777001, 1e-5
+    want = KL_KERNEL
+    if kernel == "f32":
+        monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
+        want = "policy_train_kernel<kl>"
+    pp, vp = init_policy(D, *widths, seed=61), init_value(B, D, seed=62)
+    tr = Trainer(ctx, algo="klppo", bins=B, dims=D, num_envs=N, steps=T,
+                 widths=widths, rng_state=x0, wd_policy=wd, train_grid_cap=cap)
+    tr.set_params(POLICY, pp)
+    tr.set_params(VALUE, vp)
+    orc = po.Trainer(po.OR_KLPPO, B, D, N, T,
+                     po.perbin_model(2 * D, list(widths), po.OR_SOFTMAX), pp,
+                     po.full_model(B * 2 * D, [64, 32], 1), vp, wd_pi=wd, x0=x0)
+    npi = tr.num_params(POLICY)
+    terminal_rows = 0
+    for it in range(iters):
+        orc.set_params(0, tr.params(POLICY))
+        orc.set_params(1, tr.params(VALUE))
+        orc.rollout()
+        tr.set_forced_actions(step_major(orc.buf(po.BUF_STEP_CHOICE), N, T))
+        tr.rollout()
+        tr.learn()
+        orc.learn()
+        k = tr.kernel_info()
+        assert k["policy_train"]["kernel"] == want, k
+        is_end = orc.buf(po.BUF_ROW_IS_END)
+        rows = len(is_end)
+        terminal_rows += int(rows - N * T - N) if rows > N * T + N else 0
+        dev = tr.buffer(BUF_POLICY_GRADS).reshape(-1, npi)
+        ref = np.asarray(orc.buf(po.BUF_POLICY_GRADS)).reshape(-1, npi)
+        mag = np.asarray(orc.buf(po.BUF_POLICY_GRADS_MAG)).reshape(-1, npi)
+        for ep in range(dev.shape[0]):
+            budget = {} if ep == 0 else {"p99_units": GRAD_UNITS_P99_DRIFT}
+            assert_grad_units(dev[ep], ref[ep], mag[ep],
+                              what="klppo %s B64 N%d cap%d it%d epoch%d"
+                                   % (kernel, N, cap, it, ep), **budget)
+        okl = orc.buf(po.BUF_KL).reshape(-1, 3)
+        gkl = tr.buffer(BUF_KL)
+        np.testing.assert_array_equal(gkl[:, 0], okl[:, 0])   # beta used
+        np.testing.assert_array_equal(gkl[:, 2], okl[:, 2])   # beta after
+        assert_close(gkl[:, 1], okl[:, 1], what="mean KL it%d" % it)
+        assert_close(tr.params(POLICY), orc.params(0), what="policy it%d" % it)
+    # the batches reached the terminal end rows (E_t of ended trajectories)
+    assert terminal_rows > 0, terminal_rows
+    tr.close()
