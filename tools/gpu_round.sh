@@ -19,7 +19,7 @@ for c in 2 5; do
 done
 timeout -k 10 300 python -u bench.py --rollout-steps 32 --steps 3 --warmup 1 --no-cpu-baseline > $O/bT32.log 2>&1 || { tail -5 $O/bT32.log; exit 1; }
 tail -1 $O/bT32.log > $O/profiles/${TAG}_bench_config3_T32.json
-# side line: kl_ppo_learner on the config-3 shape (the f32 train kernel)
+# side line: kl_ppo_learner on the config-3 shape (its split train kernel)
 timeout -k 10 300 python -u bench.py --algo klppo --steps 5 --warmup 1 --no-cpu-baseline > $O/bkl.log 2>&1 || { tail -5 $O/bkl.log; exit 1; }
 tail -1 $O/bkl.log > $O/profiles/${TAG}_bench_config3_klppo.json
 cut -c1-400 $O/profiles/${TAG}_bench_config*.json
