@@ -158,6 +158,11 @@ __device__ __forceinline__ int relu_bit(float x) {
   return m;
 }
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
+// XCD-aware work order (as policy_split8wh_kernels.hip: the adjacent
+// records that share a 128-byte line are read by one XCD's L2)
+#ifndef XH_4H_XCD
+#define XH_4H_XCD 1
+#endif
 
 __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     PolicyTrainArgs a) {
@@ -171,15 +176,20 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   constexpr int kKG = kTraceGroups - 1;  // the kernel-level stamps' group
   S4H_STAMP(a, kKG, w, l, 0);
   const int ngroups = a.b.T * a.b.N / 2;  // 64-row groups of two envs
-  const int J = (int)blockIdx.x < ngroups
-                    ? (ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x
-                    : 0;
+#if XH_4H_XCD
+  const int b0 = ((int)gridDim.x & 7) == 0
+                     ? ((int)blockIdx.x & 7) * ((int)gridDim.x >> 3) + ((int)blockIdx.x >> 3)
+                     : (int)blockIdx.x;
+#else
+  const int b0 = (int)blockIdx.x;
+#endif
+  const int J = b0 < ngroups ? (ngroups - b0 + (int)gridDim.x - 1) / (int)gridDim.x : 0;
   if (J == 0) return;  // uniform over the workgroup
   int gstep = (int)gridDim.x;
   // group index of this workgroup's group j (clamped: work past the end is
   // discarded); its envs are transitions 2 g and 2 g + 1 of the [T][N] arrays
   auto gindex = [&](int j) {
-    return (size_t)((int)blockIdx.x + min(j, J - 1) * gstep);
+    return (size_t)(b0 + min(j, J - 1) * gstep);
   };
 
   // wave 0 stages group j+2 during X(j): branch-free loads at its start
