@@ -507,18 +507,34 @@ __global__ __launch_bounds__(256) void mlp3_backward_data_kernel(Mlp3Bwd o, int 
 }
 
 // The three weight-gradient GEMMs of mlp_backward ([dW | db] = dY^T [X | 1],
-// split-K over the rows into slabs) in one launch: blockIdx.x enumerates
-// layer 2's tile, layer 1's two and layer 0's n0 tiles, blockIdx.z the split.
+// split-K over the rows into slabs) in one launch of ntiles x splits
+// workgroups: tile b enumerates layer 2's tile, layer 1's two and layer 0's
+// n0 tiles, z the split.  Workgroups are dispatched round-robin over the 8
+// XCDs, so (when splits % 8 == 0) XCD x runs the splits x S/8 .. (x+1) S/8 - 1
+// with all their tiles back to back: the tiles of a split read the same rows
+// of dY (layer 0's tiles the same dZ1 rows), and one L2 serves them, where
+// tile-major order spread them over several XCDs (config 3: each dZ1 row
+// fetched three times).  Every tile sums the same rows in the same order
+// either way.
 template <class LB0, class EP0>
 __global__ __launch_bounds__(256) void mlp3_weight_grad_kernel(
     ColMajor d2, RowsOnes x2, EpSlab e2, ColMajor d1, RowsOnes x1, EpSlab e1,
-    ColMajor d0, LB0 x0, EP0 e0, int N0, int K) {
+    ColMajor d0, LB0 x0, EP0 e0, int N0, int K, int ntiles, int splits) {
   __shared__ float As[BK][BM + PAD];
   __shared__ float Bs[BK][BN + PAD];
-  const int splits = gridDim.z;
+  const int L = blockIdx.x;
+  int b, z;  // uniform
+  if ((splits & 7) == 0) {
+    const int slot = L >> 3;
+    z = (L & 7) * (splits >> 3) + slot / ntiles;
+    b = slot % ntiles;
+  } else {
+    z = L / ntiles;
+    b = L % ntiles;
+  }
   int kper = (K + splits - 1) / splits;
   kper = (kper + BK - 1) / BK * BK;
-  const int k0 = blockIdx.z * kper, k1 = min(K, k0 + kper);
+  const int k0 = z * kper, k1 = min(K, k0 + kper);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lr = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
   auto out = [&](const f32x16 &acc, int M, int N, int bn, auto &ep) {
@@ -526,10 +542,9 @@ __global__ __launch_bounds__(256) void mlp3_weight_grad_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = wm * 32 + acc_row(r, h);
-      if (m < M && n < N) ep(m, n, blockIdx.z, acc[r]);
+      if (m < M && n < N) ep(m, n, z, acc[r]);
     }
   };
-  const int b = blockIdx.x;  // uniform
   if (b == 0) {
     out(gemm_tile(d2, x2, 1, kFV2 + 1, 0, 0, k0, k1, As, Bs), 1, kFV2 + 1, 0, e2);
   } else if (b < 3) {
@@ -746,9 +761,10 @@ hipError_t value_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
   const EpSlab e1{slab, stride, o1, o1 + kFV2 * kFV1, kFV1};
   const int sp = splits < 1 ? 1 : splits;
   auto run = [&](auto x0, auto e0, int N0) {
-    const dim3 grid(3 + (N0 + BN - 1) / BN, 1, sp);
-    hipLaunchKernelGGL((mlp3_weight_grad_kernel<decltype(x0), decltype(e0)>), grid,
-                       dim3(256), 0, s, d2, x2, e2, d1, x1, e1, d0, x0, e0, N0, M);
+    const int nt = 3 + (N0 + BN - 1) / BN;
+    hipLaunchKernelGGL((mlp3_weight_grad_kernel<decltype(x0), decltype(e0)>),
+                       dim3(nt * sp), dim3(256), 0, s, d2, x2, e2, d1, x1, e1, d0, x0,
+                       e0, N0, M, nt, sp);
     return hipGetLastError();
   };
   if (a.w0red) {
