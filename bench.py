@@ -324,7 +324,14 @@ def main():
     value = env_steps / dt
     # dominant kernel: policy_train (one PPO epoch over N*T env-steps);
     # algorithmic FLOPs = fwd + bwd(2x fwd) of the per-bin policy per env-step
-    flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * n * T
+    # (KL-PPO trains every row of kl_ppo_learner's state matrix: the N T
+    # transitions, N open end rows and the last iteration's n_end terminal
+    # end rows -- their count read from its done flags)
+    rows_epoch = n * T
+    if ALGO == "klppo":
+        from dependence_free_rl_amd.trainer import BUF_DONE
+        rows_epoch += n + int(np.asarray(tr.buffer(BUF_DONE)).astype(np.int64).sum())
+    flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * rows_epoch
     avg_ms = ms_pt / max(n_pt, 1)
     # what ran, and the peak of its arithmetic: from the library
     kinfo = tr.kernel_info()
@@ -348,7 +355,8 @@ def main():
     # p_old, advantage (12 B); per workgroup of the train grid (the library
     # reports it: 256 at configs 3 / 5, 512 at config 2) one f32 gradient slab
     from dependence_free_rl_amd.trainer import policy_param_count
-    alg_bytes = (n * T * (B * D + 4 + 12) +
+    # (KL-PPO rows also read their old distribution, B floats)
+    alg_bytes = (rows_epoch * (B * D + 4 + 12 + (4 * B if ALGO == "klppo" else 0)) +
                  kinfo["train_grid"] * policy_param_count(D, H1, H2) * 4)
     roofline = kernel_roofline(kt, flops_epoch, avg_ms)
     # whole-iteration HBM roofline (BASELINE metric: "fraction of the HBM
@@ -413,7 +421,8 @@ def main():
                      "clock_ghz_profiled": pmc and pmc.get("clock_ghz"),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(avg_ms, 4),
-                     "flops_per_launch": flops_epoch}),
+                     "flops_per_launch": flops_epoch,
+                     "rows_per_launch": rows_epoch}),
         "iteration_roofline": {"flops_per_env_step": it_flops,
                                "achieved": round(it_tflops, 2),
                                "unit": "TFLOP/s",
