@@ -1,7 +1,6 @@
 #!/bin/bash
-# Ad-hoc GPU check: the value step's split cap (256 = product, 512, 1024) at
-# configs 2 and 3.
+# Ad-hoc GPU check: wave-priority alternation in the 64-bin train kernel
+# (per slot / per phase) against the product, config 3.
 set -o pipefail
 export TMPDIR=/tmp
-CFG=2 ROUNDS=2 bash tools/ab_lib.sh build/vm512/libxylo_hip.so build/vm1024/libxylo_hip.so || exit 1
-CFG=3 ROUNDS=2 bash tools/ab_lib.sh build/vm512/libxylo_hip.so build/vm1024/libxylo_hip.so || exit 1
+CFG=3 ROUNDS=2 bash tools/ab_lib.sh build/v8wh_prio1/libxylo_hip.so build/v8wh_prio2/libxylo_hip.so || exit 1
