@@ -957,6 +957,10 @@ __device__ __forceinline__ void sample_step128_x(const RolloutArgs &a, int t, bo
     a.probs_out[(size_t)env * 128 + lane] = p[0];
     a.probs_out[(size_t)env * 128 + 64 + lane] = p[1];
   }
+  if (a.qold_out) {  // KL-PPO / record_distrib: every step's distribution
+    a.qold_out[((size_t)t * N + env) * 128 + lane] = p[0];
+    a.qold_out[((size_t)t * N + env) * 128 + 64 + lane] = p[1];
+  }
   int choice;
   if (a.forced) {
     choice = a.forced[(size_t)t * N + env];

@@ -28,6 +28,20 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Built twice (Makefile), as policy_split8wh_kernels.hip: the actor-critic /
+// PPO kernel, and with XH_8X_KL_TU=1 (policy_split8x_kl_kernels.o) its
+// KL-PPO form, policy_train_split8x_kl_kernel.  The KL additions are
+// preprocessor blocks, so the first object compiles from exactly its
+// measured source.
+#ifndef XH_8X_KL_TU
+#define XH_8X_KL_TU 0
+#endif
+#if XH_8X_KL_TU
+#define KLTU(...) __VA_ARGS__
+#else
+#define KLTU(...)
+#endif
+
 namespace xh {
 namespace s8x {
 
@@ -57,7 +71,12 @@ constexpr int F_XP = F_X + 4 * kD * 64;     // [4 slots][3 dims][16 li][4 rt]
 constexpr int F_IT = F_XP + 4 * kD * 64;    // [4 slots] the unit's item is item_a
 constexpr int F_REC = F_IT + 4;             // [4 slots][action, pold, adv, -]
 constexpr int F_SC = F_REC + 4 * 4;         // [16] the scales' reduction
+#if XH_8X_KL_TU
+constexpr int F_Q = F_SC + 16;              // KL-PPO: [4 slots][64 rows] old distribution
+constexpr int F_END = F_Q + 4 * 64;
+#else
 constexpr int F_END = F_SC + 16;
+#endif
 constexpr size_t kLds = L_F + sizeof(float) * F_END;
 static_assert(kLds <= 160 * 1024, "LDS");
 static_assert(F_REC % 4 == 0 && F_GW % 4 == 0 && F_GP % 4 == 0 && F_X % 4 == 0 &&
@@ -156,7 +175,15 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
 
+#if XH_8X_KL_TU
+// kl_ppo_learner's epoch over every row of its state matrix, as
+// policy_split8wh_kernels.hip's KL build: envs 0..TN-1 the transitions,
+// TN..TN+N-1 the open trajectories' end rows, then the n_end terminal end
+// rows of end_list; the two 64-row units of an env stage their halves of q.
+__global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kl_kernel(
+#else
 __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
+#endif
     PolicyTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
@@ -165,7 +192,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int l = tid & 63, G = l >> 4, li = l & 15;
+#if XH_8X_KL_TU
+  const int NT = a.b.T * a.b.N;
+  const int n_end = *a.n_end;
+  const int nenv = NT + a.b.N + n_end;
+  const float beta = *a.beta;
+#else
   const int nenv = a.b.T * a.b.N;
+#endif
   // this workgroup's envs: e_j = blockIdx.x + j gridDim.x, j < J (the host
   // caps the grid at the env count); units u < U = 2 J, u >> 1 the env, u & 1
   // the half; units past the end are clamped to the last one (layer 1 /
@@ -292,33 +326,86 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
     for (int j = 0; j < 4; ++j) accW2[ot][j] = 0.0f;
   float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float accB3 = 0.0f, w0 = 0.0f, w1 = 0.0f, w2 = 0.0f, sa = 0.0f, sb = 0.0f;
+#if XH_8X_KL_TU
+  double kl_acc = 0.0;  // sum of KL(q || p) over this wave's rows
+#endif
 
   // wave 0 stages unit u: branch-free loads (lane = row: the row's three
   // bins as a byte triple; lanes 0-2 the env's action, old probability and
   // advantage, the others the item's coordinates), then the stores into
   // slot u & 3 (bins / 8 in row order and in the C layout's order, whether
   // the item is item_a, the record)
+#if XH_8X_KL_TU
+  struct Raw {
+    int bi, rec;
+    float q;     // the old distribution's entry of row l of the unit
+    int ended;   // open end rows: step T - 1 of the env ended
+  };
+  // the row of the [T+1][N] arrays env g reads and the row of its old
+  // distribution (kind 0 transition, 1 open end row, 2 terminal end row)
+  auto kl_rows = [&](int g, size_t &ti, size_t &qi) {
+    const int N = a.b.N;
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g < NT) {
+      ti = qi = (size_t)g;
+    } else if (g < NT + N) {
+      ti = (size_t)NT + (g - NT);
+      qi = (size_t)(NT - N) + (g - NT);
+    } else {
+      const int jj = min(g - NT - N, max(n_end - 1, 0));
+      const int te = __builtin_amdgcn_readfirstlane(a.end_list[jj]);
+      ti = qi = (size_t)te;
+    }
+  };
+  auto stage_load = [&](int u) {
+    size_t ti = tindex(u), qi = 0;
+    kl_rows((int)ti, ti, qi);
+    const size_t ri = qi;
+#else
   struct Raw {
     int bi, rec;
   };
   auto stage_load = [&](int u) {
     const size_t ti = tindex(u);
+    const size_t ri = ti;
+#endif
     int lo = (uhalf(u) * 64 + l) * kD;
     asm volatile("" : "+v"(lo));
     const unsigned char *bp = reinterpret_cast<const unsigned char *>(
         a.b.bins + ti * (kB * kD) + lo);
     const int bins = (int)bp[0] | ((int)bp[1] << 8) | ((int)bp[2] << 16);
-    const int *src = l == 0   ? a.b.action + ti
-                     : l == 1 ? reinterpret_cast<const int *>(a.b.pold + ti)
-                     : l == 2 ? reinterpret_cast<const int *>(a.adv + ti)
+    const int *src = l == 0   ? a.b.action + ri
+                     : l == 1 ? reinterpret_cast<const int *>(a.b.pold + ri)
+                     : l == 2 ? reinterpret_cast<const int *>(a.adv + ri)
                               : reinterpret_cast<const int *>(a.b.items + ti * 4);
+#if XH_8X_KL_TU
+    Raw r{bins, *src, a.qold[qi * kB + uhalf(u) * 64 + l], 0};
+    const int g = __builtin_amdgcn_readfirstlane((int)tindex(u));
+    if (g >= NT && g < NT + a.b.N) r.ended = a.b.done[qi];
+    return r;
+  };
+  auto stage_store = [&](const Raw &r, int s, int u) {
+    const int g = __builtin_amdgcn_readfirstlane((int)tindex(u));
+    const int kind = g < NT ? 0 : g < NT + a.b.N ? 1 : 2;
+    // the terminal view: the chosen bin without the item (rl.h:336-343)
+    const int itm = __builtin_amdgcn_readlane(r.rec, 3);
+    const bool sub = kind == 2 && uhalf(u) * 64 + l == __builtin_amdgcn_readfirstlane(r.rec);
+    lf[F_Q + s * 64 + l] = r.q;
+#else
     return Raw{bins, *src};
   };
   auto stage_store = [&](const Raw &r, int s) {
+#endif
     const int pl = 4 * (l & 15) + (l >> 4);
 #pragma unroll
     for (int d = 0; d < kD; ++d) {
+#if XH_8X_KL_TU
+      const int bd = (signed char)((r.bi >> (8 * d)) & 0xff) -
+                     (sub ? (signed char)((itm >> (8 * d)) & 0xff) : 0);
+      const float x = (float)bd / (float)kCapacity;
+#else
       const float x = (float)(signed char)((r.bi >> (8 * d)) & 0xff) / (float)kCapacity;
+#endif
       lf[F_X + s * (kD * 64) + d * 64 + l] = x;
       lf[F_XP + s * (kD * 64) + d * 64 + pl] = x;
     }
@@ -328,7 +415,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
     for (int d = 0; d < kD; ++d)
       ia &= (signed char)((item >> (8 * d)) & 0xff) == a.env.item_a[d];
     if (l == 0) lf[F_IT + s] = ia ? 1.0f : 0.0f;
+#if XH_8X_KL_TU
+    // action (lane 0), advantage (lane 2, 0 for end rows), whether the row
+    // counts (lane 3)
+    const int ended = __builtin_amdgcn_readfirstlane(r.ended);
+    const bool valid = kind == 0 || (kind == 1 ? ended == 0 : g - NT - a.b.N < n_end);
+    if (l == 0 || l == 2) lf[F_REC + 4 * s + l] = kind == 0 ? __int_as_float(r.rec) : 0.0f;
+    if (l == 3) lf[F_REC + 4 * s + 3] = valid ? 1.0f : 0.0f;
+#else
     if (l < 3) lf[F_REC + 4 * s + l] = __int_as_float(r.rec);
+#endif
   };
   // H1 values (C layout, r-tile rt) scaled by S_H -> the two f16 part images
   auto store_h1 = [&](const f32x4 &t, int sb, int rt) {
@@ -419,9 +515,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
   f32x4 pre_v[4], pre_v1[4];
   Raw raw = {0, 0};
   if (w == 0) {
-    stage_store(stage_load(0), 0);
-    stage_store(stage_load(1), 1);
-    stage_store(stage_load(2), 2);
+    stage_store(stage_load(0), 0 KLTU(, 0));
+    stage_store(stage_load(1), 1 KLTU(, 1));
+    stage_store(stage_load(2), 2 KLTU(, 2));
   }
   __syncthreads();
   layer1_all(0, stb0);
@@ -457,6 +553,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
     const float b3 = lf[F_B3];
     const f32x4 rec = lds4v(lf + F_REC + 4 * cs);
     const float itc = lf[F_IT + cs];
+#if XH_8X_KL_TU
+    // the env's old distribution: its first unit's half, then its second's
+    const float qv0 = lf[F_Q + cs * 64 + l], qv1 = lf[F_Q + ((v + 1) & 3) * 64 + l];
+    float kp0 = 0.0f, kp1 = 0.0f, kg0 = 0.0f, kg1 = 0.0f;
+#endif
     f32x4 gx0[2], gx1[2], gx2[2];
     float ex0 = 0.0f, ex1 = 0.0f, se = 0.0f, g0 = 0.0f, g1 = 0.0f;
     f32x4 gr4, ggk[2], hT[2];
@@ -476,6 +577,26 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
         }
       } else if (k == 1) {
         if (first) se = seg_sum<64>(ex0 + ex1);
+#if XH_8X_KL_TU
+      } else if (k == 2) {
+        if (first) {
+          // kl_regulated_loss (policy_gradient.h:41-85) through
+          // softmax_layer::backward (the Jacobian's sum in the next slot);
+          // the KL sum on one wave per env, in turn
+          const int cu = __builtin_amdgcn_readfirstlane(__float_as_int(rec[0]));
+          const float Ac = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rec[2])));
+          const float rse = __builtin_amdgcn_rcpf(se);
+          kp0 = ex0 * rse;
+          kp1 = ex1 * rse;
+          kg0 = fmaf(beta, kp0 - qv0, kp0 * Ac);
+          kg1 = fmaf(beta, kp1 - qv1, kp1 * Ac);
+          if (l == cu) kg0 -= Ac;
+          if (64 + l == cu) kg1 -= Ac;
+          const bool vld = __builtin_amdgcn_readfirstlane(__float_as_int(rec[3])) != 0;
+          if (vld && ((v >> 1) & 7) == w)
+            kl_acc += (double)(qv0 * logf(qv0 / kp0)) + (double)(qv1 * logf(qv1 / kp1));
+        }
+#else
       } else if (k == 2) {
         if (first) {
           const int cu = __builtin_amdgcn_readfirstlane(__float_as_int(rec[0]));
@@ -503,8 +624,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
             if (64 + l == cu) g1 -= Ac;
           }
         }
+#endif
       } else if (k == 3) {
         if (first) {
+#if XH_8X_KL_TU
+          {
+            const float sgv = seg_sum<64>(fmaf(kp1, kg1, kp0 * kg0));
+            const bool vld = __builtin_amdgcn_readfirstlane(__float_as_int(rec[3])) != 0;
+            g0 = vld ? kp0 * (kg0 - sgv) : 0.0f;
+            g1 = vld ? kp1 * (kg1 - sgv) : 0.0f;
+          }
+#endif
           // both units' g (this wave's copies): unit v, then unit v + 1
           gw[l] = g0;
           gp[4 * (l & 15) + (l >> 4)] = g0;
@@ -580,7 +710,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
       } else if (k == 36) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 44) {
-        if (w == 0) stage_store(raw, ns);  // unit v+3's rows
+        if (w == 0) stage_store(raw, ns KLTU(, v + 3));  // unit v+3's rows
       }
     };
     f32x4 pre_v2[4];
@@ -724,6 +854,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
     }
   }
 
+#if XH_8X_KL_TU
+  {
+    // the workgroup's KL sum (the loop's last barrier is behind: F_Z is free)
+    double dv = kl_acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) dv += __shfl_xor(dv, o, kWave);
+    double *kd = reinterpret_cast<double *>(lf + F_Z);
+    if (l == 0) kd[w] = dv;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int v8 = 0; v8 < 8; ++v8) t += kd[v8];
+      a.kl_part[blockIdx.x] = t;
+    }
+  }
+#endif
+
   // ---------------------------------------------------- slab write-out ----
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
   const float *w3g = P + PL.ow3();
@@ -783,8 +931,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8x_kernel(
 
 }  // namespace s8x
 
+#if XH_8X_KL_TU
+hipError_t launch_policy_train_split8x_kl(const PolicyTrainArgs &a, int grid,
+                                          hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)s8x::policy_train_split8x_kl_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s8x::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(s8x::policy_train_split8x_kl_kernel, dim3(grid),
+                     dim3(s8x::kThreads), s8x::kLds, s, a);
+  return hipGetLastError();
+}
+#else
 hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s) {
+  if (a.algo == kKLPPO) return launch_policy_train_split8x_kl(a, grid, s);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)s8x::policy_train_split8x_kernel,
@@ -796,5 +960,6 @@ hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
                      dim3(s8x::kThreads), s8x::kLds, s, a);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace xh

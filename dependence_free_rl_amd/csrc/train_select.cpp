@@ -5,6 +5,7 @@
 //   64 bins, 2-D, [128,128] (configs 3 / 4)  policy_train_split8wh_kernel
 //                                  (KL-PPO: policy_train_split8wh_kl_kernel)
 //   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
+//                                  (KL-PPO: policy_train_split8x_kl_kernel)
 //   32 bins, 1-D, [64,64] (config 2)         policy_train_split4h_kernel
 // and the f32-MFMA kernels of policy_kernels.hip for every other shape (KL-PPO
 // included), and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
@@ -50,9 +51,11 @@ static bool train_kernel_is(const char *name) {
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
   const bool algo = a.algo == kPPO || a.algo == kAC;
-  // KL-PPO: the 64-bin 2-D kernel only (its KL instantiation)
+  // KL-PPO: the KL builds of the 64-bin 2-D and 128-bin 3-D kernels
   if (a.algo == kKLPPO)
-    return H1 == 128 && H2 == 128 && a.env.B == 64 && a.env.D == 2;
+    return H1 == 128 && H2 == 128 &&
+           ((a.env.B == 64 && a.env.D == 2) ||
+            (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims));
   if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
     return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
   return algo && H1 == 128 && H2 == 128 &&
@@ -72,7 +75,8 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
   }
   if (a.env.B == kSplit128Bins) {
     if (!ov) {
-      info->name = "policy_train_split8x_kernel";
+      info->name = a.algo == kKLPPO ? "policy_train_split8x_kl_kernel"
+                                    : "policy_train_split8x_kernel";
       return launch_policy_train_split8x(a, grid, s);
     }
 #if XH_VARIANT_KERNELS

@@ -383,6 +383,10 @@ hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
+// its KL-PPO build (policy_split8x_kl_kernels.o; called by
+// launch_policy_train_split8x)
+hipError_t launch_policy_train_split8x_kl(const PolicyTrainArgs &a, int grid,
+                                          hipStream_t s);
 int policy_train_grid(int B, int D, int H1, int H2, int kl);
 hipError_t launch_eval_argmax(const EvalArgs &a, int H1, int H2,
                               hipStream_t s);

@@ -1391,8 +1391,12 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     if (c.algo == XH_PG) return create_pg(ctx, c, out);
     if (c.algo != XH_PPO && c.algo != XH_AC && c.algo != XH_KLPPO)
       return fail(XH_ERR_INVALID, "algo %d", c.algo);
-    if (c.algo == XH_KLPPO && c.bins > 64)
-      return fail(XH_ERR_INVALID, "KL-PPO: bins %d > 64 not supported",
+    // KL-PPO beyond 64 bins: the 128-bin 3-D [128,128] shape's split train
+    // kernel only (the f32 KL kernel is written for <= 64 bins)
+    if (c.algo == XH_KLPPO && c.bins > 64 &&
+        !(c.bins == 128 && c.dims == 3 && c.policy_h1 == 128 && c.policy_h2 == 128))
+      return fail(XH_ERR_INVALID,
+                  "KL-PPO: bins %d > 64 supported at 128 bins, 3-D, [128,128] only",
                   c.bins);
     if (!xh::policy_shape_supported(c.bins, c.dims, c.policy_h1, c.policy_h2))
       return fail(XH_ERR_INVALID,

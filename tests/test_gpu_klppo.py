@@ -1,4 +1,4 @@
-"""KL-PPO on the 64-bin f16-pair train kernel, against the oracle.
+"""KL-PPO on the f16-pair train kernels (64 and 128 bins), against the oracle.
 
 kl_ppo_learner (/root/reference/xylo/policy_gradient.h:310-335) trains on
 every row of its state matrix: the transitions, the open trajectories' end
@@ -6,7 +6,8 @@ rows and the terminal end rows (rl.h:336-343), with kl_regulated_loss
 (policy_gradient.h:41-85) and beta adapted between epochs from the mean KL.
 At the 64-bin 2-D [128,128] shape (BASELINE config 3's) the epoch runs
 policy_train_split8wh_kl_kernel, the KL-PPO build of the headline train
-kernel (f16 pairs + the exact bf16 split).  Lockstep iterations: the oracle learns from the
+kernel, and at the 128-bin 3-D shape (config 5's) policy_train_split8x_kl_kernel
+(f16 pairs + the exact bf16 split).  Lockstep iterations: the oracle learns from the
 device trainer's parameters each iteration, samples its own actions and the
 device replays them, so the comparison measures one learn()'s arithmetic.
 Several iterations carry the envs into terminal end rows (a 64-bin episode
@@ -22,22 +23,24 @@ from gpu_helpers import step_major
 
 pytestmark = pytest.mark.gpu
 
-KL_KERNEL = "policy_train_split8wh_kl_kernel"
+KL_KERNEL = {64: "policy_train_split8wh_kl_kernel", 128: "policy_train_split8x_kl_kernel"}
 
 
-@pytest.mark.parametrize("N,T,iters,cap,kernel",
-                         [(48, 4, 5, 0, "split"), (32, 4, 4, 1, "split"),
-                          (48, 4, 5, 0, "f32")],
-                         ids=["n48", "n32_cap1", "n48_f32"])
-def test_klppo_split_matches_oracle(ctx, monkeypatch, N, T, iters, cap, kernel):
+@pytest.mark.parametrize("B,D,N,T,iters,cap,kernel",
+                         [(64, 2, 48, 4, 5, 0, "split"), (64, 2, 32, 4, 4, 1, "split"),
+                          (64, 2, 48, 4, 5, 0, "f32"),
+                          (128, 3, 24, 8, 5, 0, "split"), (128, 3, 24, 8, 5, 1, "split")],
+                         ids=["b64_n48", "b64_n32_cap1", "b64_n48_f32", "b128_n24",
+                              "b128_n24_cap1"])
+def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, kernel):
     """kernel "f32": the same iterations on the f32-MFMA KL kernel
     (XH_TRAIN_KERNEL=f32), the accuracy reference the split kernel's logged
     error units are read against."""
     from oracle import pyoracle as po
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import BUF_KL, BUF_POLICY_GRADS
-    B, D, widths, x0, wd = 64, 2, (128, 128), 777001, 1e-5
-    want = KL_KERNEL
+    widths, x0, wd = (128, 128), 777001, 1e-5
+    want = KL_KERNEL[B]
     if kernel == "f32":
         monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
         want = "policy_train_kernel<kl>"
@@ -70,8 +73,8 @@ def test_klppo_split_matches_oracle(ctx, monkeypatch, N, T, iters, cap, kernel):
         for ep in range(dev.shape[0]):
             budget = {} if ep == 0 else {"p99_units": GRAD_UNITS_P99_DRIFT}
             assert_grad_units(dev[ep], ref[ep], mag[ep],
-                              what="klppo %s B64 N%d cap%d it%d epoch%d"
-                                   % (kernel, N, cap, it, ep), **budget)
+                              what="klppo %s B%d N%d cap%d it%d epoch%d"
+                                   % (kernel, B, N, cap, it, ep), **budget)
         okl = orc.buf(po.BUF_KL).reshape(-1, 3)
         gkl = tr.buffer(BUF_KL)
         np.testing.assert_array_equal(gkl[:, 0], okl[:, 0])   # beta used
