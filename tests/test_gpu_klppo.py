@@ -84,3 +84,28 @@ def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, ke
     # the batches reached the terminal end rows (E_t of ended trajectories)
     assert terminal_rows > 0, terminal_rows
     tr.close()
+
+
+@pytest.mark.parametrize("B,D,widths", [(64, 2, (128, 128)), (128, 3, (128, 128))])
+def test_recorded_distributions(ctx, B, D, widths):
+    """record_distrib (the composed learner's q, rl.h:27-30) on the split
+    rollouts: every step's distribution sums to 1, the last step's equals the
+    probabilities output, and each step's p_old is its entry at the chosen
+    bin."""
+    from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
+    from dependence_free_rl_amd.trainer import BUF_ACTION, BUF_POLD, BUF_PROBS, BUF_QOLD
+    N, T = 32, 4
+    tr = Trainer(ctx, algo="ac" if B == 128 else "ppo", bins=B, dims=D, num_envs=N,
+                 steps=T, widths=widths, rng_state=99001, record_distrib=True)
+    tr.set_params(POLICY, init_policy(D, *widths, seed=71))
+    tr.set_params(VALUE, init_value(B, D, seed=72))
+    tr.rollout()
+    q = tr.buffer(BUF_QOLD)
+    assert q.shape == (T, N, B)
+    np.testing.assert_allclose(q.sum(axis=2), 1.0, rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(q[T - 1], tr.buffer(BUF_PROBS))
+    act = tr.buffer(BUF_ACTION)
+    pold = tr.buffer(BUF_POLD)
+    pick = np.take_along_axis(q, act[:, :, None].astype(np.int64), axis=2)[:, :, 0]
+    np.testing.assert_array_equal(pick, pold)
+    tr.close()
