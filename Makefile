@@ -15,7 +15,8 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \
-            $(SRC)/policy_split4h_kernels.o $(SRC)/loss_kernels.o \
+            $(SRC)/policy_split4h_kernels.o $(SRC)/policy_split4h_kl_kernels.o \
+            $(SRC)/loss_kernels.o \
             $(SRC)/train_select.o $(SRC)/model_api.o $(SRC)/xylo_hip.o
 # superseded train kernels (the config-3 / config-5
 # epoch's earlier forms), kept for A/B runs in the variant library only
@@ -61,7 +62,7 @@ FLAGS_policy_split8wg_kernels := -mllvm -amdgpu-mfma-vgpr-form
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@
 
-# the KL-PPO builds of the 64- and 128-bin train kernels (their own objects:
+# the KL-PPO builds of the 64-, 128- and 32-bin train kernels (their own objects:
 # the full unroll of their task lambdas needs a threshold the other builds
 # are not made with, policy_split8wh_kernels.hip)
 $(SRC)/policy_split8wh_kl_kernels.o: $(SRC)/policy_split8wh_kernels.hip $(HDRS)
@@ -69,6 +70,9 @@ $(SRC)/policy_split8wh_kl_kernels.o: $(SRC)/policy_split8wh_kernels.hip $(HDRS)
 	    -mllvm -pragma-unroll-threshold=200000 -c $< -o $@
 $(SRC)/policy_split8x_kl_kernels.o: $(SRC)/policy_split8x_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_policy_split8x_kernels) -DXH_8X_KL_TU=1 \
+	    -mllvm -pragma-unroll-threshold=200000 -c $< -o $@
+$(SRC)/policy_split4h_kl_kernels.o: $(SRC)/policy_split4h_kernels.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(FLAGS_policy_split4h_kernels) -DXH_4H_KL_TU=1 \
 	    -mllvm -pragma-unroll-threshold=200000 -c $< -o $@
 
 $(SRC)/xylo_hip.o: $(SRC)/xylo_hip.cpp $(HDRS)

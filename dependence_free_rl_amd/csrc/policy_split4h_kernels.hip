@@ -26,6 +26,20 @@
 #include "xh_kernels.h"
 #include "xh_split.h"
 
+// Built twice (Makefile), as policy_split8wh_kernels.hip: the PPO /
+// actor-critic kernel, and with XH_4H_KL_TU=1 (policy_split4h_kl_kernels.o)
+// its KL-PPO form, policy_train_split4h_kl_kernel; the KL additions are
+// preprocessor blocks, so the first object compiles from exactly its
+// measured source.
+#ifndef XH_4H_KL_TU
+#define XH_4H_KL_TU 0
+#endif
+#if XH_4H_KL_TU
+#define KLTU(...) __VA_ARGS__
+#else
+#define KLTU(...)
+#endif
+
 // Phase stamps (trace build, tools/build_trace4h.sh: -DXH_DIAG_TRACE=1, run
 // with XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
 // workgroups records the cycle counter at 0 X start, 1 layer 2 (+ group j's
@@ -75,7 +89,12 @@ constexpr int F_IT = F_XP + 3 * 64;      // [3 slots][2 envs] item is item_a (+ 
 constexpr int F_REC = F_IT + 8;          // [3 slots][2 envs][action, pold, adv, -]
 constexpr int F_SC = F_REC + 3 * 8;      // [16] the scales' reduction
 constexpr int F_W3G = F_SC + 16;         // [64] w3 (the slab write-out's)
+#if XH_4H_KL_TU
+constexpr int F_Q = F_W3G + kH;          // KL-PPO: [3 slots][64 rows] old distribution
+constexpr int F_END = F_Q + 3 * 64;
+#else
 constexpr int F_END = F_W3G + kH;
+#endif
 constexpr size_t kLds = L_F + sizeof(float) * F_END;
 static_assert(2 * kLds <= 160 * 1024, "LDS: two workgroups per CU");
 static_assert(F_REC % 4 == 0 && F_GW % 4 == 0 && F_GP % 4 == 0 && F_X % 4 == 0 &&
@@ -164,8 +183,18 @@ __device__ __forceinline__ int relu_bit(float x) {
 #define XH_4H_XCD 1
 #endif
 
+#if XH_4H_KL_TU
+// kl_ppo_learner's epoch over every row of its state matrix (rows 0..TN-1
+// the transitions, TN..TN+N-1 the open trajectories' end rows, then the
+// n_end terminal end rows of end_list), two rows per 64-row group: each
+// half resolves its own row, kind and validity (the last group's second
+// half may lie past the rows: not valid).
+__global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kl_kernel(
+    PolicyTrainArgs a) {
+#else
 __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     PolicyTrainArgs a) {
+#endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
   const PolicyLayout PL{kF0, kH, kH};
@@ -175,7 +204,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   const int l = tid & 63, G = l >> 4, li = l & 15;
   constexpr int kKG = kTraceGroups - 1;  // the kernel-level stamps' group
   S4H_STAMP(a, kKG, w, l, 0);
+#if XH_4H_KL_TU
+  const int NT = a.b.T * a.b.N;
+  const int n_end = *a.n_end;
+  const int nrows = NT + a.b.N + n_end;
+  const int ngroups = (nrows + 1) / 2;  // 64-row groups of two rows
+  const float beta = *a.beta;
+#else
   const int ngroups = a.b.T * a.b.N / 2;  // 64-row groups of two envs
+#endif
 #if XH_4H_XCD
   const int b0 = ((int)gridDim.x & 7) == 0
                      ? ((int)blockIdx.x & 7) * ((int)gridDim.x >> 3) + ((int)blockIdx.x >> 3)
@@ -195,13 +232,70 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   // wave 0 stages group j+2 during X(j): branch-free loads at its start
   // (lane = row: its bin; lanes 0-2 / 3-5 env A's / B's action, old
   // probability and advantage, lanes 6 / 7 their items), the stores late
+#if XH_4H_KL_TU
+  struct Raw {
+    int bi, rec;
+    float q;     // the old distribution's entry of this lane's row and bin
+    int ended;   // this lane's half, an open end row: step T - 1 ended
+  };
+  // row r of the learner's state matrix: its row of the [T+1][N] arrays and
+  // of its old distribution, its kind (0 transition, 1 open end row, 2
+  // terminal end row) and whether it counts (r is wave-uniform)
+  auto kl_row = [&](int r, size_t &ti, size_t &qi, int &kind, bool &inr) {
+    const int N = a.b.N;
+    r = __builtin_amdgcn_readfirstlane(r);
+    inr = r < nrows;
+    if (r < NT) {
+      ti = qi = (size_t)r;
+      kind = 0;
+    } else if (r < NT + N) {
+      ti = (size_t)NT + (r - NT);
+      qi = (size_t)(NT - N) + (r - NT);
+      kind = 1;
+    } else {
+      const int jj = r - NT - N;
+      const int te = jj < n_end ? __builtin_amdgcn_readfirstlane(a.end_list[jj]) : 0;
+      ti = qi = (size_t)te;
+      kind = 2;
+    }
+  };
+#else
   struct Raw {
     int bi, rec;
   };
+#endif
   // (every wave loads -- the loads are tiny -- and only wave 0 stores: no
   // branch around the loads, whose results then stay in flight until the
   // store; the byte is sign-extended there, and the record address is chosen
   // by selects, not branches)
+#if XH_4H_KL_TU
+  auto stage_load = [&](int j) {
+    const int g = (int)gindex(j);
+    size_t tA, qA, tB, qB;
+    int kA, kB2;
+    bool iA, iB;
+    kl_row(2 * g, tA, qA, kA, iA);
+    kl_row(2 * g + 1, tB, qB, kB2, iB);
+    const bool eB = l >= 32;
+    const size_t tl = eB ? tB : tA, ql = eB ? qB : qA;
+    const int bins = (int)*reinterpret_cast<const unsigned char *>(a.b.bins + tl * 32 + (l & 31));
+    // the record lanes: 0-2 row A's action, p_old, advantage (rows of the
+    // [T][N] arrays: the old distribution's), 3-5 row B's, 6 / 7 the items
+    const size_t ri = (l >= 3 && l != 6) ? qB : qA;
+    const int k = l % 3;
+    const unsigned long long p0 = (unsigned long long)(a.b.action + ri);
+    const unsigned long long p1 = (unsigned long long)(a.b.pold + ri);
+    const unsigned long long p2 = (unsigned long long)(a.adv + ri);
+    const unsigned long long p3 = (unsigned long long)(a.b.items + ((l & 1) ? tB : tA) * 4);
+    unsigned long long pa = k == 1 ? p1 : p2;
+    pa = k == 0 ? p0 : pa;
+    pa = l >= 6 ? p3 : pa;
+    Raw r{bins, *reinterpret_cast<const int *>(pa), a.qold[ql * 32 + (l & 31)], 0};
+    const bool open = eB ? kB2 == 1 : kA == 1;
+    if (open) r.ended = a.b.done[ql];
+    return r;
+  };
+#else
   auto stage_load = [&](int j) {
     const size_t g = gindex(j);
     int lo = l;
@@ -218,6 +312,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     pa = l >= 6 ? p3 : pa;
     return Raw{bins, *reinterpret_cast<const int *>(pa)};
   };
+#endif
   // ---- prologue: every global load first (the scales' inputs, the small
   // parameters, this lane's W2 / W2' fragment values), then the scales
   // (every workgroup the same), then the f16 pairs of tile w
@@ -334,9 +429,34 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     for (int j = 0; j < 4; ++j) accW2[ot][j] = 0.0f;
   float accW3[4] = {0.0f, 0.0f, 0.0f, 0.0f}, accB2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float accB3 = 0.0f, w0 = 0.0f, sa = 0.0f, sb = 0.0f;
+#if XH_4H_KL_TU
+  double kl_acc = 0.0;  // sum of KL(q || p) over this wave's rows
+#endif
 
+#if XH_4H_KL_TU
+  auto stage_store = [&](const Raw &r, int s, int j) {
+    const int g = (int)gindex(j);
+    size_t tA, qA, tB, qB;
+    int kA, kB2;
+    bool iA, iB;
+    kl_row(2 * g, tA, qA, kA, iA);
+    kl_row(2 * g + 1, tB, qB, kB2, iB);
+    const bool eB = l >= 32;
+    // the terminal view: the chosen bin without the item (rl.h:336-343)
+    const int cA = __builtin_amdgcn_readlane(r.rec, 0), cB = __builtin_amdgcn_readlane(r.rec, 3);
+    const int iA8 = __builtin_amdgcn_readlane(r.rec, 6), iB8 = __builtin_amdgcn_readlane(r.rec, 7);
+    const bool sub = (eB ? kB2 : kA) == 2 && (l & 31) == (eB ? cB : cA);
+    const int bv = (signed char)(r.bi & 0xff) - (sub ? (signed char)((eB ? iB8 : iA8) & 0xff) : 0);
+    const float x = (float)bv / (float)kCapacity;
+    lf[F_Q + s * 64 + l] = r.q;
+    // each half's validity (its own lanes' r.ended)
+    const int endA = __builtin_amdgcn_readlane(r.ended, 0), endB = __builtin_amdgcn_readlane(r.ended, 32);
+    const bool vA = iA && (kA == 0 || (kA == 1 ? endA == 0 : true));
+    const bool vB = iB && (kB2 == 0 || (kB2 == 1 ? endB == 0 : true));
+#else
   auto stage_store = [&](const Raw &r, int s) {
     const float x = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
+#endif
     lf[F_X + s * 64 + l] = x;
     lf[F_XP + s * 64 + 4 * (l & 15) + (l >> 4)] = x;
     const int itA = __builtin_amdgcn_readlane(r.rec, 6);
@@ -345,7 +465,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       lf[F_IT + 2 * s] = (signed char)(itA & 0xff) == a.env.item_a[0] ? 1.0f : 0.0f;
       lf[F_IT + 2 * s + 1] = (signed char)(itB & 0xff) == a.env.item_a[0] ? 1.0f : 0.0f;
     }
+#if XH_4H_KL_TU
+    // the records: action and advantage of a transition, 0 for end rows;
+    // slots 3 / 7 whether the row counts
+    if (l == 0 || l == 2) lf[F_REC + 8 * s + l] = kA == 0 ? __int_as_float(r.rec) : 0.0f;
+    if (l == 3 || l == 5)
+      lf[F_REC + 8 * s + 4 + l - 3] = kB2 == 0 ? __int_as_float(r.rec) : 0.0f;
+    if (l == 6) lf[F_REC + 8 * s + 3] = vA ? 1.0f : 0.0f;
+    if (l == 7) lf[F_REC + 8 * s + 7] = vB ? 1.0f : 0.0f;
+#else
     if (l < 6) lf[F_REC + 8 * s + (l >= 3 ? 4 + l - 3 : l)] = __int_as_float(r.rec);
+#endif
   };
   // H1 values (C layout, r-tile rt) scaled by S_H -> the two f16 part images
   auto store_h1 = [&](const f32x4 &t, int sb, int rt) {
@@ -434,8 +564,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   f32x4 pre_cur[4];
   Raw raw = {0, 0};
   if (w == 0) {
-    stage_store(raw0, 0);
-    stage_store(raw1, 1);
+    stage_store(raw0, 0 KLTU(, 0));
+    stage_store(raw1, 1 KLTU(, 1));
   }
   __syncthreads();
   layer1_all(0, stb0);
@@ -462,6 +592,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     const float b3 = lf[F_B3];
     const f32x4 recA = lds4v(lf + F_REC + 8 * cs), recB = lds4v(lf + F_REC + 8 * cs + 4);
     const float itA = lf[F_IT + 2 * cs], itB = lf[F_IT + 2 * cs + 1];
+#if XH_4H_KL_TU
+    const float qv = lf[F_Q + cs * 64 + l];
+    float kp = 0.0f, kg = 0.0f;
+#endif
     f32x4 gx0[2];
     float ex = 0.0f, se = 0.0f, gz = 0.0f;
     f32x4 gr4, ggk[2], hT[2];
@@ -474,6 +608,26 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
         ex = __expf(((z4[0] + z4[1]) + (z4[2] + z4[3])) + b3);
       } else if (k == 1) {
         se = seg_sum<32>(ex);  // per env (32-lane segment)
+#if XH_4H_KL_TU
+      } else if (k == 2) {
+        // kl_regulated_loss (policy_gradient.h:41-85) through
+        // softmax_layer::backward (the Jacobian's sum in the next slot), per
+        // 32-lane row; the KL sum on one wave per group, in turn
+        const int cA = __builtin_amdgcn_readfirstlane(__float_as_int(recA[0]));
+        const int cB = __builtin_amdgcn_readfirstlane(__float_as_int(recB[0]));
+        const bool eB = l >= 32;
+        const int c = eB ? cB : cA;
+        const float Ac = __int_as_float(__builtin_amdgcn_readfirstlane(
+                             __float_as_int(recA[2]))) * (eB ? 0.0f : 1.0f) +
+                         __int_as_float(__builtin_amdgcn_readfirstlane(
+                             __float_as_int(recB[2]))) * (eB ? 1.0f : 0.0f);
+        kp = ex * __builtin_amdgcn_rcpf(se);
+        kg = fmaf(beta, kp - qv, kp * Ac);
+        if ((l & 31) == c) kg -= Ac;
+        const bool vA = __builtin_amdgcn_readfirstlane(__float_as_int(recA[3])) != 0;
+        const bool vB = __builtin_amdgcn_readfirstlane(__float_as_int(recB[3])) != 0;
+        if ((j & 3) == w && (eB ? vB : vA)) kl_acc += (double)(qv * logf(qv / kp));
+#else
       } else if (k == 2) {
         const int cA = __builtin_amdgcn_readfirstlane(__float_as_int(recA[0]));
         const int cB = __builtin_amdgcn_readfirstlane(__float_as_int(recB[0]));
@@ -505,7 +659,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
           gz = p * Ac;
           if ((l & 31) == c) gz -= Ac;
         }
+#endif
       } else if (k == 3) {
+#if XH_4H_KL_TU
+        {
+          const float sgv = seg_sum<32>(kp * kg);
+          const bool vA = __builtin_amdgcn_readfirstlane(__float_as_int(recA[3])) != 0;
+          const bool vB = __builtin_amdgcn_readfirstlane(__float_as_int(recB[3])) != 0;
+          gz = (l >= 32 ? vB : vA) ? kp * (kg - sgv) : 0.0f;
+        }
+#endif
         gw[l] = gz;
         gp[4 * (l & 15) + (l >> 4)] = gz;
         accB3 += gz;  // wave 0's is written out
@@ -559,7 +722,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
       } else if (k == 20) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
       } else if (k == 22) {
-        if (w == 0) stage_store(raw, ns);  // group j+2's rows
+        if (w == 0) stage_store(raw, ns KLTU(, j + 2));  // group j+2's rows
       }
     };
     f32x4 pre_nx[4];
@@ -718,6 +881,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
   }
   S4H_STAMP(a, kKG, w, l, 2);
 
+#if XH_4H_KL_TU
+  {
+    // the workgroup's KL sum (the loop's last barrier is behind: F_Z is free)
+    double dv = kl_acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) dv += __shfl_xor(dv, o, kWave);
+    double *kd = reinterpret_cast<double *>(lf + F_Z);
+    if (l == 0) kd[w] = dv;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int v4 = 0; v4 < kNW; ++v4) t += kd[v4];
+      a.kl_part[blockIdx.x] = t;
+    }
+  }
+#endif
+
   // ---------------------------------------------------- slab write-out ----
   float *slab = a.slab + (size_t)blockIdx.x * a.slab_stride;
   const float *w3g = lf + F_W3G;
@@ -767,8 +948,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
 
 }  // namespace s4h
 
+#if XH_4H_KL_TU
+hipError_t launch_policy_train_split4h_kl(const PolicyTrainArgs &a, int grid,
+                                          hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)s4h::policy_train_split4h_kl_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s4h::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(s4h::policy_train_split4h_kl_kernel, dim3(grid),
+                     dim3(s4h::kThreads), s4h::kLds, s, a);
+  return hipGetLastError();
+}
+#else
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s) {
+  if (a.algo == kKLPPO) return launch_policy_train_split4h_kl(a, grid, s);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)s4h::policy_train_split4h_kernel,
@@ -780,5 +977,6 @@ hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
                      dim3(s4h::kThreads), s4h::kLds, s, a);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace xh

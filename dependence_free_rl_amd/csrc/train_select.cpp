@@ -7,6 +7,7 @@
 //   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
 //                                  (KL-PPO: policy_train_split8x_kl_kernel)
 //   32 bins, 1-D, [64,64] (config 2)         policy_train_split4h_kernel
+//                                  (KL-PPO: policy_train_split4h_kl_kernel)
 // and the f32-MFMA kernels of policy_kernels.hip for every other shape (KL-PPO
 // included), and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
 // kernels' tests).
@@ -51,11 +52,13 @@ static bool train_kernel_is(const char *name) {
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
   const bool algo = a.algo == kPPO || a.algo == kAC;
-  // KL-PPO: the KL builds of the 64-bin 2-D and 128-bin 3-D kernels
+  // KL-PPO: the KL builds of the 64-bin 2-D, 128-bin 3-D and 32-bin 1-D
+  // [64,64] kernels (two rows per group there, any row count)
   if (a.algo == kKLPPO)
-    return H1 == 128 && H2 == 128 &&
-           ((a.env.B == 64 && a.env.D == 2) ||
-            (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims));
+    return (H1 == 128 && H2 == 128 &&
+            ((a.env.B == 64 && a.env.D == 2) ||
+             (a.env.B == kSplit128Bins && a.env.D == kSplit128Dims))) ||
+           (H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1);
   if (algo && H1 == 64 && H2 == 64 && a.env.B == kSplit4hBins && a.env.D == 1)
     return (a.b.T * a.b.N) % 2 == 0;  // 64-row groups of two envs
   return algo && H1 == 128 && H2 == 128 &&
@@ -70,7 +73,8 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
   info->math = kMathSplitTrainF16;
   const char *ov = train_override();
   if (a.env.B == kSplit4hBins) {
-    info->name = "policy_train_split4h_kernel";
+    info->name = a.algo == kKLPPO ? "policy_train_split4h_kl_kernel"
+                                  : "policy_train_split4h_kernel";
     return launch_policy_train_split4h(a, grid, s);
   }
   if (a.env.B == kSplit128Bins) {

@@ -381,6 +381,10 @@ hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
+// its KL-PPO build (policy_split4h_kl_kernels.o; called by
+// launch_policy_train_split4h)
+hipError_t launch_policy_train_split4h_kl(const PolicyTrainArgs &a, int grid,
+                                          hipStream_t s);
 hipError_t launch_policy_train_split8x(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 // its KL-PPO build (policy_split8x_kl_kernels.o; called by

@@ -1,4 +1,4 @@
-"""KL-PPO on the f16-pair train kernels (64 and 128 bins), against the oracle.
+"""KL-PPO on the f16-pair train kernels (64, 128 and 32 bins), against the oracle.
 
 kl_ppo_learner (/root/reference/xylo/policy_gradient.h:310-335) trains on
 every row of its state matrix: the transitions, the open trajectories' end
@@ -6,8 +6,10 @@ rows and the terminal end rows (rl.h:336-343), with kl_regulated_loss
 (policy_gradient.h:41-85) and beta adapted between epochs from the mean KL.
 At the 64-bin 2-D [128,128] shape (BASELINE config 3's) the epoch runs
 policy_train_split8wh_kl_kernel, the KL-PPO build of the headline train
-kernel, and at the 128-bin 3-D shape (config 5's) policy_train_split8x_kl_kernel
-(f16 pairs + the exact bf16 split).  Lockstep iterations: the oracle learns from the
+kernel, at the 128-bin 3-D shape (config 5's) policy_train_split8x_kl_kernel
+and at the 32-bin 1-D [64,64] shape (config 2's, two rows per 64-row group)
+policy_train_split4h_kl_kernel (f16 pairs + the exact bf16 split, DESIGN.md
+§3.0a-d).  Lockstep iterations: the oracle learns from the
 device trainer's parameters each iteration, samples its own actions and the
 device replays them, so the comparison measures one learn()'s arithmetic.
 Several iterations carry the envs into terminal end rows (a 64-bin episode
@@ -23,15 +25,18 @@ from gpu_helpers import step_major
 
 pytestmark = pytest.mark.gpu
 
-KL_KERNEL = {64: "policy_train_split8wh_kl_kernel", 128: "policy_train_split8x_kl_kernel"}
+KL_KERNEL = {64: "policy_train_split8wh_kl_kernel", 128: "policy_train_split8x_kl_kernel",
+             32: "policy_train_split4h_kl_kernel"}
 
 
 @pytest.mark.parametrize("B,D,N,T,iters,cap,kernel",
                          [(64, 2, 48, 4, 5, 0, "split"), (64, 2, 32, 4, 4, 1, "split"),
                           (64, 2, 48, 4, 5, 0, "f32"),
-                          (128, 3, 24, 8, 5, 0, "split"), (128, 3, 24, 8, 5, 1, "split")],
+                          (128, 3, 24, 8, 5, 0, "split"), (128, 3, 24, 8, 5, 1, "split"),
+                          (32, 1, 64, 4, 5, 0, "split"), (32, 1, 48, 4, 5, 1, "split"),
+                          (32, 1, 64, 4, 5, 0, "f32")],
                          ids=["b64_n48", "b64_n32_cap1", "b64_n48_f32", "b128_n24",
-                              "b128_n24_cap1"])
+                              "b128_n24_cap1", "b32_n64", "b32_n48_cap1", "b32_n64_f32"])
 def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, kernel):
     """kernel "f32": the same iterations on the f32-MFMA KL kernel
     (XH_TRAIN_KERNEL=f32), the accuracy reference the split kernel's logged
@@ -39,7 +44,7 @@ def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, ke
     from oracle import pyoracle as po
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import BUF_KL, BUF_POLICY_GRADS
-    widths, x0, wd = (128, 128), 777001, 1e-5
+    widths, x0, wd = ((64, 64) if B == 32 else (128, 128)), 777001, 1e-5
     want = KL_KERNEL[B]
     if kernel == "f32":
         monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
