@@ -74,7 +74,8 @@ int xh_ctx_inject_fault(xh_ctx *ctx, int kind);
 /* XH_KLPPO: kl_ppo_learner (policy_gradient.h:310-335, ppo2_training.cc):
  * PPO's k = 4 full-batch epochs with kl_regulated_loss and an adaptive beta
  * that carries over from one learn() to the next.  Per-bin shapes with
- * bins <= 64. */
+ * bins <= 64, and 128 bins 3-D [128,128] (the split train kernel only: a
+ * batch holding an overflowed bin fails its learn() there). */
 /* XH_PG: policy_gradient_learner = REINFORCE (policy_gradient.h:88-147,
  * bp::pg_learner, pg_training.cc) with a FULL-layer policy
  * full(4B, policy_h1) - relu [- full(policy_h1, policy_h2) - relu] -
