@@ -446,10 +446,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   // item_a, the record) late in the same phase, so the loads' latency hides
   // under layer 2
 #if XH_8WH_KL_TU
+  // (the old distribution goes straight to its LDS slot by an LDS-direct
+  // load, and an open end row's done byte rides in lane 1's record word:
+  // no registers held across layer 2 for either)
   struct Raw {
     int bi, rec;
-    float q;     // the old distribution's entry of bin l
-    int ended;   // open end rows: step T - 1 of the env ended
   };
   // the row of the [T+1][N] arrays group g reads and the row of its old
   // distribution (kind 0 transition, 1 open end row, 2 terminal end row); g
@@ -491,17 +492,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     // coordinates), so nothing waits for it before its use
     // (the address chosen by selects, not branches)
     const unsigned long long p0 = (unsigned long long)(a.b.action + ri);
+#if XH_8WH_KL_TU
+    // lane 1: the aligned word holding done[qi] (an open end row's validity)
+    const unsigned long long p1 =
+        (unsigned long long)(a.b.done + (qi & ~(size_t)3));
+#else
     const unsigned long long p1 = (unsigned long long)(a.b.pold + ri);
+#endif
     const unsigned long long p2 = (unsigned long long)(a.adv + ri);
     const unsigned long long p3 = (unsigned long long)(a.b.items + ti * 4);
     unsigned long long pa = l >= 3 ? p3 : p2;
     pa = l == 1 ? p1 : pa;
     pa = l == 0 ? p0 : pa;
 #if XH_8WH_KL_TU
-    Raw r{bins, *reinterpret_cast<const int *>(pa), a.qold[qi * kB + l], 0};
-    const int g = __builtin_amdgcn_readfirstlane((int)tindex(j));
-    if (g >= NT && g < NT + a.b.N) r.ended = a.b.done[qi];
-    return r;
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    __builtin_amdgcn_global_load_lds((gvoid *)(a.qold + qi * kB + l),
+                                     (lvoid *)(lf + F_Q + ((int)(j % 3)) * 64), 4, 0, 0);
+    return Raw{bins, *reinterpret_cast<const int *>(pa)};
   };
   auto stage_store = [&](const Raw &r, int s, int j) {
     const int g = __builtin_amdgcn_readfirstlane((int)tindex(j));
@@ -513,7 +521,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     const int b1 = (signed char)((r.bi >> 8) & 0xff) - (sub ? (signed char)((itm >> 8) & 0xff) : 0);
     const float x0 = (float)b0 / (float)kCapacity;
     const float x1 = (float)b1 / (float)kCapacity;
-    lf[F_Q + s * 64 + l] = r.q;
+    // the old distribution's LDS-direct load (issued with this group's
+    // staging loads, long done): complete before the phase's barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
     return Raw{bins, *reinterpret_cast<const int *>(pa)};
   };
@@ -534,7 +544,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     // the record: action (lane 0), advantage (lane 2, 0 for end rows), whether
     // the row counts (lane 3: not a terminal row past n_end, nor an open end
     // row whose env ended at step T - 1)
-    const int ended = __builtin_amdgcn_readfirstlane(r.ended);
+    const int dw = __builtin_amdgcn_readlane(r.rec, 1);
+    const size_t qi1 = kind == 1 ? (size_t)(NT - a.b.N) + (g - NT) : 0;
+    const int ended = (dw >> (8 * (int)(qi1 & 3))) & 0xff;
     const bool valid = kind == 0 || (kind == 1 ? ended == 0 : g - NT - a.b.N < n_end);
     if (l == 0 || l == 2) lf[F_REC + 4 * s + l] = kind == 0 ? __int_as_float(r.rec) : 0.0f;
     if (l == 3) lf[F_REC + 4 * s + 3] = valid ? 1.0f : 0.0f;
