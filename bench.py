@@ -178,31 +178,152 @@ def cpu_baseline():
                 n_env, T, iters)}
 
 
-def pmc_traffic(kernel="policy_train", any_shape=False):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
-    FETCH_SIZE / WRITE_SIZE summary (separate --pmc passes; see
-    tools/pmc_summary.py): 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read
-    correction measured for 1- to 16-byte lanes by tools/probes/fetch_probe.hip
-    (older summaries without the calibration are converted here)."""
+def library_sha256():
+    """sha256 of the libxylo_hip.so this process loaded (the build the PMC
+    summaries must have profiled to be cited)."""
+    import hashlib
+    from dependence_free_rl_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE summary (separate --pmc passes; tools/pmc_summary.py):
+    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read correction measured for 1- to
+    16-byte lanes by tools/probes/fetch_probe.hip.
+
+    Only a summary of THIS library build is cited: its "_meta".library_sha256
+    must equal `lib_sha` (the sha256 of the loaded libxylo_hip.so; a summary
+    of another build -- older kernels -- gives None).  Among matching
+    summaries the newest by its recorded creation time wins, and only a
+    summary of this very shape counts (PShape<B, D, H1, H2> for the f32
+    kernels; the split kernels have one shape each)."""
     import glob
-    # newest round first (profiles/<round><pass>[_c<config>]_pmc_summary.json);
-    # only a summary of this very shape counts (PShape<B, D, H1, H2>)
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")),
-                   reverse=True)
     shape = "PShape<%d, %d, %d, %d>" % (B, D, H1, H2)
-    for path in files:
+    best = None
+    for path in glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")):
         with open(path) as f:
             summ = json.load(f)
+        meta = summ.get("_meta", {})
+        if lib_sha is None or meta.get("library_sha256") != lib_sha:
+            continue
         # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
         s = next((v for k, v in sorted(summ.items())
                   if k.startswith(kernel) and (any_shape or shape in v.get("kernel", ""))
                   and "hbm_bytes" in v), None)
-        if s:
-            hbm = s["hbm_bytes"]
-            if "hbm_bytes_raw_reads" not in s:  # pre-calibration summary
-                hbm = s["fetch_bytes_x2"] + s["write_bytes"]
-            return hbm, os.path.relpath(path, REPO), s
-    return None, None, None
+        if s and (best is None or meta.get("created", "") > best[0]):
+            best = (meta.get("created", ""), s["hbm_bytes"],
+                    os.path.relpath(path, REPO), s)
+    if best is None:
+        return None, None, None
+    return best[1], best[2], best[3]
+
+
+# bytes one venv step moves per env (venv_kernels.hip venv_step_kernel, mode
+# 1): the bins read and written (B*D int8 each), the action read (4), the
+# item record read and written (4 + 4), the engine state read and written
+# (4 + 4), the reward (4) and done (1) written
+def venv_bytes_per_env_step():
+    return 2 * B * D + 4 + 8 + 8 + 4 + 1
+
+
+def env_only(args, cfg, ctx, rank, world, rdzv):
+    """--env-only: the env half of the path alone:
+    xh_venv_step -- agent::step minus react for every env in ONE kernel
+    (bin_packing.h:53-70, rl.h:325-349) -- over the config's env batch, each
+    env replaying a fixed bin choice (uploaded once; an env overflows its
+    bin within a few steps and resets, so apply, the item draws and reset
+    all run), streams in reference order with a sampling policy's 2 draws
+    skipped per step.  HBM-bound: `roofline` is HBM GB/s of venv_step_kernel
+    (algorithmic bytes / HIP-event launch time) against 8 TB/s.  Beside it,
+    the reference's first-fit heuristic agent (firstfit_agent.cc:10-28) on
+    the device evaluator, whole episodes with the state in registers."""
+    from dependence_free_rl_amd.trainer import heuristic_evaluate
+    from dependence_free_rl_amd.venv import VecEnv
+    n = args.envs or cfg["N"]
+    env = VecEnv(ctx, n, bins=B, dims=D, rng_state=20241008, env_offset=n * rank,
+                 num_envs_global=n * world, policy_draws=2)
+    env.set_actions(np.random.default_rng(1234 + rank).integers(0, B, n))
+    for _ in range(args.warmup):
+        env.step(fetch=False)
+    env.synchronize()
+    if rdzv:
+        rdzv.barrier()
+    env.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        env.step(fetch=False)
+    env.synchronize()
+    if rdzv:
+        rdzv.barrier()
+    dt = time.perf_counter() - t0
+    if rdzv:
+        dt = rdzv.allreduce_max(dt)
+    ms, launches = env.kernel_time()
+    env.set_timing(False)
+    avg_ms = ms / max(launches, 1)
+    reward, done = env.get(_venv_reward()), env.get(_venv_done())
+    env.close()
+    value = n * world * args.steps / dt
+    bytes_launch = n * venv_bytes_per_env_step()
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic, traffic_src, _ = pmc_traffic("venv_step_kernel<%d, %d>" % (B, D),
+                                          any_shape=True,
+                                          lib_sha=library_sha256())
+    # the first-fit agent: 4 episodes of every env on the device evaluator
+    # (its own kernel, whole episodes with the env state in registers)
+    ff = heuristic_evaluate(ctx, "firstfit", B, D, n, 4, 20241008 + rank)
+    ff_steps = int(ff["steps"].sum())
+    line = {
+        "metric": "env-steps/sec (whole node) bin-packing env step, %d-bin "
+                  "%d-D, env only" % (B, D),
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic (fixed-size bin-packing instances; every env "
+                "replays a fixed random bin choice)",
+        "config": {"workload": "env only (xh_venv_step) on the env batch of "
+                               "BASELINE config %d: %d envs/GPU, %d bins, %d-D"
+                               % (args.config, n, B, D),
+                   "envs_per_gpu": n, "bins": B, "dims": D,
+                   "parallelism": "dp%d" % world},
+        "roofline": {"kernel": "venv_step_kernel<%d, %d>" % (B, D),
+                     "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": bytes_launch,
+                     "bytes_per_env_step": venv_bytes_per_env_step(),
+                     "avg_launch_ms": round(avg_ms, 5)},
+        "health": {"done_rate": float(done.mean()),
+                   "reward_mean": float(reward.mean())},
+        "firstfit_agent": {
+            "env_steps_per_s": round(ff_steps / (ff["elapsed_ms"] * 1e-3), 1)
+            if ff["elapsed_ms"] > 0 else None,
+            "env_steps": ff_steps, "episodes": 4 * n,
+            "mean_episode_reward": float(ff["totals"].sum() / (4 * n)),
+            "device_ms": round(ff["elapsed_ms"], 3),
+            "source": "xh_heuristic_evaluate (firstfit_agent.cc:10-28), "
+                      "HIP events around its launch"},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+def _venv_reward():
+    from dependence_free_rl_amd._lib import VENV_REWARD
+    return VENV_REWARD
+
+
+def _venv_done():
+    from dependence_free_rl_amd._lib import VENV_DONE
+    return VENV_DONE
 
 
 def main():
@@ -225,6 +346,9 @@ def main():
                     help="learner on the config's shape (default: the "
                          "config's; klppo = kl_ppo_learner, a side line, not "
                          "the headline)")
+    ap.add_argument("--env-only", action="store_true",
+                    help="the env step alone (xh_venv_step over the config's "
+                         "env batch, HBM roofline) instead of training")
     ap.add_argument("--reference-lr", action="store_true",
                     help="raw lr on row sums as the reference (diverges at "
                          "this batch size; default: lr_scale_rows)")
@@ -271,6 +395,12 @@ def main():
     from dependence_free_rl_amd import (POLICY, VALUE, Context, Trainer,
                                         init_policy, init_value, runtime_info)
     ctx = Context(device=device, rank=rank, world=world, uid=uid)
+    if args.env_only:
+        env_only(args, cfg, ctx, rank, world, rdzv)
+        ctx.close()
+        if rdzv:
+            rdzv.close()
+        return
     n = args.envs or cfg["N"]
     # lr_scale_rows: the reference applies its raw lr to row SUMS (nn.h:
     # 94-98, 624); at this batch (N*T*B rows per epoch) that diverges to
@@ -305,13 +435,22 @@ def main():
     if rdzv:
         dt = rdzv.allreduce_max(dt)
 
-    # numerical health of what was timed (after the timed region): finite
-    # parameters / probabilities, done rate and mean episode length
-    health = tr.health()
     ms_pt, n_pt = tr.kernel_time("policy_train")
+    # KL-PPO trains every row of kl_ppo_learner's state matrix: the N T
+    # transitions, N open end rows and the n_end terminal end rows of the
+    # batch -- read from the done flags of the LAST TIMED iteration, before
+    # the phase pass below overwrites them (the other timed iterations' counts
+    # are not kept; they differ by a fraction of a percent)
+    n_end = None
+    if ALGO == "klppo":
+        from dependence_free_rl_amd.trainer import BUF_DONE
+        n_end = int(np.asarray(tr.buffer(BUF_DONE)).astype(np.int64).sum())
+    # the phase pass also records the last step's probabilities (diagnostics,
+    # off inside the timed region) for the health check after it
     # the phase breakdown: PHASE_ITERS more iterations (every rank), every
     # launch timed
     tr.set_timing(True)
+    tr.set_record_last_step(True)
     tr.iterate(1)  # (the events' own first use)
     tr.reset_timing()
     tr.iterate(PHASE_ITERS)
@@ -320,6 +459,9 @@ def main():
           for k in ("rollout_step", "policy_train", "value", "reduce_sgd",
                     "allreduce")}
     tr.set_timing(False)
+    # numerical health (after the timed region): finite parameters and
+    # last-step probabilities, done rate and mean episode length
+    health = tr.health()
     env_steps = n * world * T * args.steps
     value = env_steps / dt
     # dominant kernel: policy_train (one PPO epoch over N*T env-steps);
@@ -329,8 +471,7 @@ def main():
     # end rows -- their count read from its done flags)
     rows_epoch = n * T
     if ALGO == "klppo":
-        from dependence_free_rl_amd.trainer import BUF_DONE
-        rows_epoch += n + int(np.asarray(tr.buffer(BUF_DONE)).astype(np.int64).sum())
+        rows_epoch += n + n_end
     flops_epoch = 3.0 * policy_fwd_flops_per_env_step() * rows_epoch
     avg_ms = ms_pt / max(n_pt, 1)
     # what ran, and the peak of its arithmetic: from the library
@@ -344,8 +485,10 @@ def main():
     split = kt["math"] != "f32_mfma"
     # the split kernels have one shape each: their summaries are keyed by
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
-    traffic, traffic_src, pmc = (pmc_traffic(kt["kernel"], any_shape=True)
-                                 if split else pmc_traffic())
+    lib_sha = library_sha256()
+    traffic, traffic_src, pmc = (
+        pmc_traffic(kt["kernel"], any_shape=True, lib_sha=lib_sha) if split
+        else pmc_traffic(lib_sha=lib_sha))
     if args.rollout_steps and args.rollout_steps != cfg["T"]:
         # the PMC passes profile the config's own T: their bytes per launch
         # are not this launch's
@@ -417,6 +560,7 @@ def main():
         "roofline": dict(roofline, **{
                      "traffic": traffic,
                      "traffic_source": traffic_src,
+                     "library_sha256": lib_sha,
                      "mfma_busy_frac": pmc and pmc.get("mfma_busy_frac"),
                      "clock_ghz_profiled": pmc and pmc.get("clock_ghz"),
                      "algorithmic_bytes_per_launch": alg_bytes,

@@ -41,7 +41,7 @@ class Config(C.Structure):
         ("rng_state", C.c_uint32), ("kl_beta", C.c_float),
         ("kl_target", C.c_float), ("adv_normalize", C.c_int),
         ("lr_scale_rows", C.c_int), ("train_grid_cap", C.c_int),
-        ("record_distrib", C.c_int)]
+        ("record_distrib", C.c_int), ("record_last_step", C.c_int)]
 
 
 class Eval(C.Structure):
@@ -111,6 +111,9 @@ def _load():
         "xh_venv_reset": (i, [vp, i]),
         "xh_venv_observe": (i, [vp]),
         "xh_venv_synchronize": (i, [vp]),
+        "xh_venv_set_timing": (i, [vp, i]),
+        "xh_venv_kernel_time": (i, [vp, C.POINTER(C.c_double),
+                                    C.POINTER(C.c_long)]),
         "xh_model_eval": (i, [vp, vp, i, vp, sz, vp, i, i, vp, sz,
                               C.POINTER(C.c_int)]),
         "xh_model_forward": (i, [vp, vp, i, vp, sz, vp, i, i, vp, sz,
@@ -123,6 +126,7 @@ def _load():
         "xh_optimizer_apply": (i, [vp, i, C.c_float, C.c_float, C.c_float,
                                    C.c_float, C.c_float, vp, vp, vp, vp, sz]),
         "xh_trainer_forget": (i, [vp]),
+        "xh_trainer_set_record_last_step": (i, [vp, i]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

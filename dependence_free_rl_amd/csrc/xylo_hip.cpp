@@ -113,6 +113,11 @@ struct xh_trainer {
   uint32_t jump_mul = 1;
   int rgrid = 0;
   bool need_shift = false;
+  // a rollout window exists that no learn() / forget() has consumed yet
+  // (xh_trainer_forget refuses to shift without one)
+  bool rolled = false;
+  // XH_BUF_LOGITS / XH_BUF_PROBS hold a recorded rollout step
+  bool last_step_recorded = false;
   // xh_trainer_set_env_state: states the next rollout starts from, keyed by
   // env (B*D bin bytes then D item bytes), applied after the forget() shift
   std::map<int, std::vector<int8_t>> env_override;
@@ -172,6 +177,10 @@ struct xh_venv {
   size_t bytes[XH_VENV_BUF_COUNT] = {};
   int *err = nullptr;
   bool counted = false;
+  // xh_venv_set_timing: HIP events around every step / apply / reset /
+  // observe launch on the context's stream
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
 
   xh::VenvArgs args() const {
     xh::VenvArgs a{};
@@ -607,8 +616,10 @@ int do_rollout(xh_trainer *t) {
   // -capacity, or an item outside the item table (set_buffer; the split
   // rollouts fold the item into per-entry biases)
   a.wide = t->bins_wide[0] || !t->items_ok[0];
-  a.logits_out = t->logits;
-  a.probs_out = t->probs;
+  // diagnostics only (tests, health checks): off in the product path
+  a.logits_out = t->cfg.record_last_step ? t->logits : nullptr;
+  a.probs_out = t->cfg.record_last_step ? t->probs : nullptr;
+  if (t->cfg.record_last_step) t->last_step_recorded = true;
   CHK(timed(t, "rollout_step", [&]() {
     return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
                                    t->rgrid, s, &t->last_rollout);
@@ -617,6 +628,7 @@ int do_rollout(xh_trainer *t) {
     t->items_ok[step + 1] = 1;  // items drawn from the table (get_item)
     t->bins_wide[step + 1] = 0;  // apply + reset on game over: bins >= 0
   }
+  t->rolled = true;
   return XH_OK;
 }
 
@@ -929,6 +941,7 @@ int do_learn(xh_trainer *t) {
     }
   }
   t->need_shift = true;
+  t->rolled = false;
   return XH_OK;
 }
 
@@ -1113,6 +1126,7 @@ int do_pg_rollout(xh_trainer *t) {
     return fail(XH_ERR_STATE, "REINFORCE rollout: %d envs still playing after "
                 "the step bound %d", *pg.host_active, t->Tb);
   pg.slot_end = steps;
+  t->rolled = true;
   return XH_OK;
 }
 
@@ -1153,6 +1167,7 @@ int do_pg_learn(xh_trainer *t) {
   CHK(reduce_and_step(t, XH_POLICY, t->pslab, t->pslab_n, t->pslab_stride,
                       t->np, t->pgrads, t->pp));
   t->need_shift = true;
+  t->rolled = false;
   return XH_OK;
 }
 
@@ -1636,6 +1651,14 @@ int xh_trainer_set_learning_rate(xh_trainer *t, int which, float lr) {
   });
 }
 
+int xh_trainer_set_record_last_step(xh_trainer *t, int on) {
+  return guard([&]() -> int {
+    if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    t->cfg.record_last_step = on ? 1 : 0;
+    return XH_OK;
+  });
+}
+
 int xh_trainer_rollout(xh_trainer *t) {
   return guard([&]() -> int {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
@@ -1655,7 +1678,14 @@ int xh_trainer_learn(xh_trainer *t) {
 int xh_trainer_forget(xh_trainer *t) {
   return guard([&]() -> int {
     if (!t) return fail(XH_ERR_INVALID, "null trainer");
+    // replay_buffer::forget() keeps the last state of the open trajectories
+    // of a window that exists: without a rollout since the last learn() /
+    // forget() there is none, and slot T holds no start states to shift
+    if (!t->rolled)
+      return fail(XH_ERR_STATE, "forget: no rollout since the last learn() / "
+                  "forget()");
     t->need_shift = true;  // as at the end of do_learn / do_pg_learn
+    t->rolled = false;
     return XH_OK;
   });
 }
@@ -1702,6 +1732,10 @@ int xh_trainer_get_buffer(xh_trainer *t, int which, void *host, size_t bytes) {
     if (!want || bytes != want)
       return fail(XH_ERR_INVALID, "buffer %d: %zu bytes, expected %zu", which,
                   bytes, want);
+    if ((which == XH_BUF_LOGITS || which == XH_BUF_PROBS) &&
+        t->cfg.algo != XH_PG && !t->last_step_recorded)
+      return fail(XH_ERR_STATE, "buffer %d: no rollout recorded its last step "
+                  "(xh_config.record_last_step is off)", which);
     HIPCHK(hipSetDevice(t->ctx->device));
     HIPCHK(copy_to_host(host, buffer_ptr(t, which), bytes, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));
@@ -1995,6 +2029,12 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
 }
 
 // ------------------------------------------------------------------ venv --
+}  // extern "C"
+namespace {
+void venv_drop_events(xh_venv *v);
+}  // namespace
+extern "C" {
+
 int xh_venv_create(xh_ctx *ctx, int num_envs, int bins, int dims,
                    uint32_t rng_state, int env_offset, int num_envs_global,
                    int policy_draws, xh_venv **out) {
@@ -2059,6 +2099,7 @@ int xh_venv_destroy(xh_venv *v) {
     if (!v) return XH_OK;
     (void)hipSetDevice(v->ctx->device);
     (void)hipStreamSynchronize(v->ctx->stream);
+    venv_drop_events(v);
     for (void *p : v->buf)
       if (p) (void)hipFree(p);
     if (v->err) (void)hipFree(v->err);
@@ -2099,10 +2140,25 @@ int venv_launch(xh_venv *v, int op, int mode, bool use_mask, bool obs) {
   a.obs = obs ? (float *)v->buf[XH_VENV_OBS] : nullptr;
   if (op == xh::kVenvObserve) a.obs = (float *)v->buf[XH_VENV_OBS];
   if (mode == 0) a.reward = nullptr;
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (v->timing) {
+    HIPCHK(hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence));
+    v->events.push_back(ev);
+    HIPCHK(hipEventRecord(ev.first, v->ctx->stream));
+  }
   const hipError_t e = xh::launch_venv(a, op, v->ctx->stream);
   if (e != hipSuccess)
     return fail(XH_ERR_HIP, "venv launch: %s", hipGetErrorString(e));
+  if (v->timing) HIPCHK(hipEventRecord(ev.second, v->ctx->stream));
   return XH_OK;
+}
+void venv_drop_events(xh_venv *v) {
+  for (auto &ev : v->events) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  v->events.clear();
 }
 }  // namespace
 
@@ -2172,6 +2228,34 @@ int xh_venv_observe(xh_venv *v) {
   return guard([&]() -> int {
     if (!v) return fail(XH_ERR_INVALID, "null venv");
     return venv_launch(v, xh::kVenvObserve, 0, false, true);
+  });
+}
+
+int xh_venv_set_timing(xh_venv *v, int on) {
+  return guard([&]() -> int {
+    if (!v) return fail(XH_ERR_INVALID, "null venv");
+    HIPCHK(hipSetDevice(v->ctx->device));
+    HIPCHK(hipStreamSynchronize(v->ctx->stream));
+    venv_drop_events(v);
+    v->timing = on != 0;
+    return XH_OK;
+  });
+}
+
+int xh_venv_kernel_time(xh_venv *v, double *ms, long *launches) {
+  return guard([&]() -> int {
+    if (!v || !ms || !launches) return fail(XH_ERR_INVALID, "null arg");
+    HIPCHK(hipSetDevice(v->ctx->device));
+    HIPCHK(hipStreamSynchronize(v->ctx->stream));
+    double total = 0;
+    for (auto &ev : v->events) {
+      float e = 0;
+      HIPCHK(hipEventElapsedTime(&e, ev.first, ev.second));
+      total += e;
+    }
+    *ms = total;
+    *launches = (long)v->events.size();
+    return XH_OK;
   });
 }
 

@@ -318,7 +318,8 @@ class Trainer:
                  lr_policy=None, lr_value=None, wd_policy=None, wd_value=None,
                  gamma=0.99, lam=0.95, clip_eps=0.2, rng_state=1,
                  num_envs_global=None, env_offset=0, adv_normalize=False,
-                 lr_scale_rows=False, train_grid_cap=0, record_distrib=False):
+                 lr_scale_rows=False, train_grid_cap=0, record_distrib=False,
+                 record_last_step=False):
         cfg = _lib.Config()
         a = ALGOS[algo]
         _lib.lib.xh_config_default(C.byref(cfg), a, bins, dims, num_envs, steps)
@@ -344,6 +345,9 @@ class Trainer:
         # test-only: cap on the train workgroups (accumulation depth tests)
         cfg.train_grid_cap = int(train_grid_cap)
         cfg.record_distrib = int(bool(record_distrib))
+        # diagnostics: the last slot's logits / probabilities (BUF_LOGITS,
+        # BUF_PROBS); off in the product path
+        cfg.record_last_step = int(bool(record_last_step))
         self.cfg = cfg
         self.ctx = ctx
         self.B, self.D, self.N, self.T = bins, dims, num_envs, steps
@@ -382,6 +386,12 @@ class Trainer:
         check(_lib.lib.xh_trainer_set_learning_rate(self.h, which, lr))
 
     # -------------------------------------------------------------- loop --
+    def set_record_last_step(self, on):
+        """Record the last rollout step's logits / probabilities (BUF_LOGITS,
+        BUF_PROBS) from the next rollout on (xh_trainer_set_record_last_step)."""
+        check(_lib.lib.xh_trainer_set_record_last_step(self.h, int(bool(on))))
+        self.cfg.record_last_step = int(bool(on))
+
     def rollout(self):
         check(_lib.lib.xh_trainer_rollout(self.h))
 
@@ -463,16 +473,21 @@ class Trainer:
 
     def health(self):
         """Numerical health of the training state (host copies, call outside
-        any timed region): finite parameters and last-step probabilities,
-        and the last batch's done rate / mean episode length (every episode
-        ends on exactly one done step)."""
+        any timed region): finite parameters and last-step probabilities
+        (when a rollout recorded them: record_last_step), and the last
+        batch's done rate / mean episode length (every episode ends on
+        exactly one done step)."""
         pp, pv = self.params(POLICY), self.params(VALUE)
         out = {"finite": bool(np.isfinite(pp).all() and np.isfinite(pv).all())}
         if self.cfg.algo != XH_PG:
-            probs = self.buffer(BUF_PROBS)
             done = self.buffer(BUF_DONE)
-            out["finite"] = out["finite"] and bool(np.isfinite(probs).all())
-            out["max_prob"] = float(probs.max())
+            try:
+                probs = self.buffer(BUF_PROBS)
+            except _lib.XhError:
+                probs = None  # no rollout recorded its last step
+            if probs is not None:
+                out["finite"] = out["finite"] and bool(np.isfinite(probs).all())
+                out["max_prob"] = float(probs.max())
             rate = float(done.mean())
             out["done_rate"] = rate
             out["mean_episode_len"] = (1.0 / rate) if rate > 0 else None

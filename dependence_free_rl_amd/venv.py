@@ -96,6 +96,17 @@ class VecEnv:
     def synchronize(self):
         check(_lib.lib.xh_venv_synchronize(self.h))
 
+    def set_timing(self, on):
+        """HIP events around every later launch (xh_venv_set_timing); drops
+        the events recorded so far."""
+        check(_lib.lib.xh_venv_set_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self):
+        """(milliseconds, launches) of the timed launches."""
+        ms, n = C.c_double(), C.c_long()
+        check(_lib.lib.xh_venv_kernel_time(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def close(self):
         if self.h:
             check(_lib.lib.xh_venv_destroy(self.h))

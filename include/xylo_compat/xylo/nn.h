@@ -366,8 +366,26 @@ class model {
   vector gradient(const std::vector<matrix> &input, const matrix &target) const {
     if (input.size() < layers_.size())
       throw xeno::error("model::gradient: one input matrix per layer");
+    // a fused device learn() may hold newer parameters than the layers
+    const_cast<model *>(this)->sync_from_device();
     vector result({parameter_size()});
     const std::size_t rows = layers_.empty() ? 0 : input[0].num_rows();
+    // every input of the chain and the target: rows x the chain's widths
+    // (the device call reads them by these sizes)
+    if (!layers_.empty()) {
+      std::size_t w = input[0].num_cols();
+      for (std::size_t i = 0; i < layers_.size(); ++i) {
+        if (input[i].num_rows() != rows || input[i].num_cols() != w)
+          throw xeno::error(xeno::string::strcat(
+              "model::gradient: input ", i, " is ", input[i].num_rows(), 'x',
+              input[i].num_cols(), ", expected ", rows, 'x', w));
+        w = layers_[i]->output_cols(w);
+      }
+      if (target.num_rows() != rows || target.num_cols() != w)
+        throw xeno::error(xeno::string::strcat(
+            "model::gradient: target is ", target.num_rows(), 'x',
+            target.num_cols(), ", expected ", rows, 'x', w));
+    }
     if (!device_chain() || !rows) {
       matrix backprop = target;
       std::size_t off = result.size();

@@ -129,6 +129,12 @@ typedef struct {
      host from the layer / loss pieces below whose loss reads it
      (discrete_action::distrib, rl.h:27-30).  0 (default): only p_old. */
   int record_distrib;
+  /* 1: the rollout also writes the last slot's logits and probabilities
+     (XH_BUF_LOGITS / XH_BUF_PROBS: [N][B] f32 each, 16.8 MB per iteration at
+     config 3) for tests and health checks.  0 (default): the product path
+     writes neither, and reading those buffers fails with XH_ERR_STATE.
+     xh_trainer_set_record_last_step changes it between iterations. */
+  int record_last_step;
 } xh_config;
 
 /* Fill `c` with the reference defaults (ppo_training.cc) for B bins, D dims. */
@@ -166,6 +172,10 @@ int xh_trainer_set_optimizer(xh_trainer *t, int which, int kind, float lr,
  * step counter) is kept. */
 int xh_trainer_set_learning_rate(xh_trainer *t, int which, float lr);
 
+/* Turn the last-step logits / probabilities record (xh_config.
+ * record_last_step) on or off from the next rollout on. */
+int xh_trainer_set_record_last_step(xh_trainer *t, int on);
+
 /* One iteration's rollout: T steps of every env (one kernel per step). */
 int xh_trainer_rollout(xh_trainer *t);
 /* learn(): value step, advantages, `epochs` policy steps; then the batch's
@@ -192,8 +202,9 @@ enum {
   XH_BUF_ADV = 9,      /* f32   [T][N]  advantages                           */
   XH_BUF_VALUE_GRAD = 10,  /* f32 [value params]  last value gradient        */
   XH_BUF_POLICY_GRADS = 11,/* f32 [epochs][policy params]                    */
-  XH_BUF_LOGITS = 12,  /* f32   [N][B]  logits of the last rollout step      */
-  XH_BUF_PROBS = 13,   /* f32   [N][B]  probabilities of the last step       */
+  XH_BUF_LOGITS = 12,  /* f32   [N][B]  logits of the last rollout step
+                                  (xh_config.record_last_step)              */
+  XH_BUF_PROBS = 13,   /* f32   [N][B]  probabilities of the last step (idem) */
   XH_BUF_V_STATE0 = 14,/* f32   [T+1][N] V(S_t) before the value step        */
   XH_BUF_QOLD = 15,    /* f32   [T][N][B] sampled distributions (KL-PPO, or
                                   xh_config.record_distrib)                  */
@@ -335,6 +346,12 @@ int xh_venv_reset(xh_venv *v, int use_mask);
 int xh_venv_observe(xh_venv *v);
 /* Waits for the venv's work; XH_ERR_INVALID if an action was out of range. */
 int xh_venv_synchronize(xh_venv *v);
+/* Kernel timing: on != 0 brackets every later step / apply / reset /
+ * observe launch with HIP events on the context's stream (and drops the
+ * events recorded so far); xh_venv_kernel_time returns their accumulated
+ * milliseconds and the launch count. */
+int xh_venv_set_timing(xh_venv *v, int on);
+int xh_venv_kernel_time(xh_venv *v, double *ms, long *launches);
 
 /* ------------------------------------------------------ model::eval -- */
 /* xylo::model::eval (nn.h:473-479) of a layer chain on the device: rows x

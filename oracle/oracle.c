@@ -771,6 +771,16 @@ void or_trainer_set_env_streams(or_trainer *t, uint64_t stride,
   }
 }
 
+/* Explicit per-env stream states (the envs are kept): env i draws from xs[i]
+ * from the next rollout on.  A sample of envs [off, off + N) of a larger
+ * reference-order job: xs[i] = the engine state at global env off + i's first
+ * draw of the iteration (2 Ng + 4 T (off + i) after x0). */
+void or_trainer_set_stream_states(or_trainer *t, const uint32_t *xs) {
+  free(t->xs);
+  t->xs = (uint32_t *)malloc(sizeof(uint32_t) * t->N);
+  memcpy(t->xs, xs, sizeof(uint32_t) * t->N);
+}
+
 const uint32_t *or_trainer_env_streams(const or_trainer *t) { return t->xs; }
 
 static uint32_t *env_rng(or_trainer *t, int i) {

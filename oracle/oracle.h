@@ -131,6 +131,8 @@ uint32_t or_trainer_rng(const or_trainer *t);
 void or_trainer_set_env_streams(or_trainer *t, uint64_t stride,
                                 int reconstruct);
 const uint32_t *or_trainer_env_streams(const or_trainer *t);
+/* Explicit per-env stream states xs[N] (envs kept), from the next rollout. */
+void or_trainer_set_stream_states(or_trainer *t, const uint32_t *xs);
 void or_trainer_get_params(const or_trainer *t, int which, float *out);
 void or_trainer_set_params(or_trainer *t, int which, const float *in);
 /* Introspection of the last rollout / learn (valid until the next call). */

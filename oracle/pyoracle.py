@@ -282,6 +282,15 @@ class Trainer:
         l.or_trainer_set_env_streams.argtypes = [C.c_void_p, C.c_uint64, C.c_int]
         l.or_trainer_set_env_streams(self.h, stride, 1 if reconstruct else 0)
 
+    def set_stream_states(self, xs):
+        """Env i draws from stream state xs[i] from the next rollout on (the
+        envs are kept): a sample of a larger reference-order job."""
+        xs = np.ascontiguousarray(xs, np.uint32)
+        assert xs.size == self.N
+        l = lib()
+        l.or_trainer_set_stream_states.argtypes = [C.c_void_p, C.c_void_p]
+        l.or_trainer_set_stream_states(self.h, _ptr(xs))
+
     def env_streams(self):
         l = lib()
         l.or_trainer_env_streams.restype = C.POINTER(C.c_uint32)

@@ -24,6 +24,16 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 
 
+def log_record(name, rec):
+    """Append one JSON line to gpurun_out/<name> (when that directory
+    exists: the GPU box's results, copied into profiles/ per round)."""
+    import json
+    d = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, name), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
 def assert_close(x, y, tol=RTOL, what=""):
     x = np.asarray(x, np.float64)
     y = np.asarray(y, np.float64)

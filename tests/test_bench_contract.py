@@ -44,13 +44,41 @@ def test_flops_match_survey_8d(bench):
 
 def test_pmc_traffic_only_for_the_same_shape(bench):
     bench.select_config(3)
-    t, src, _ = bench.pmc_traffic()
-    if t is not None:  # a committed summary of the 64-bin shape
+    sha = bench.library_sha256()
+    t, src, _ = bench.pmc_traffic(lib_sha=sha)
+    if t is not None:  # a committed summary of this build at the 64-bin shape
         assert src.startswith("profiles/") and t > 0
     bench.select_config(5)
-    t5, _, _ = bench.pmc_traffic()
+    t5, _, _ = bench.pmc_traffic(lib_sha=sha)
     # never the 64-bin kernel's counters for the 128-bin shape
     assert t5 is None or t5 != t
+
+
+def test_pmc_traffic_only_for_this_library_build(bench, tmp_path, monkeypatch):
+    """A PMC summary is cited only when its recorded library sha256 is the
+    loaded library's: another build's summary (or one without the record)
+    gives traffic None, whatever its file name."""
+    import json
+    bench.select_config(3)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"kernel": "void xh::policy_train8_kernel<xh::PShape<64, 2, 128, 128>>()",
+             "hbm_bytes": 123.0}
+    for name, meta in (("r99z_c3", {"library_sha256": "0" * 64,
+                                    "created": "2099-01-01T00:00:00+00:00"}),
+                       ("r99y_c3", None)):
+        summ = {"policy_train8_kernel": entry}
+        if meta:
+            summ["_meta"] = meta
+        (prof / ("%s_pmc_summary.json" % name)).write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    assert bench.pmc_traffic(lib_sha="f" * 64) == (None, None, None)
+    summ = {"policy_train8_kernel": dict(entry, hbm_bytes=7.0),
+            "_meta": {"library_sha256": "f" * 64,
+                      "created": "2026-01-01T00:00:00+00:00"}}
+    (prof / "r00a_c3_pmc_summary.json").write_text(json.dumps(summ))
+    t, src, _ = bench.pmc_traffic(lib_sha="f" * 64)
+    assert t == 7.0 and src == "profiles/r00a_c3_pmc_summary.json"
 
 
 def test_roofline_math_comes_from_the_library(bench):

@@ -98,7 +98,7 @@ def test_overflowed_start_states_run_the_f32_kernels(ctx, monkeypatch, B, D,
             monkeypatch.delenv("XH_TRAIN_KERNEL", raising=False)
             monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
-                     widths=widths, rng_state=77)
+                     widths=widths, rng_state=77, record_last_step=True)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         bins, items = tr.env_state()

@@ -101,7 +101,8 @@ def test_recorded_distributions(ctx, B, D, widths):
     from dependence_free_rl_amd.trainer import BUF_ACTION, BUF_POLD, BUF_PROBS, BUF_QOLD
     N, T = 32, 4
     tr = Trainer(ctx, algo="ac" if B == 128 else "ppo", bins=B, dims=D, num_envs=N,
-                 steps=T, widths=widths, rng_state=99001, record_distrib=True)
+                 steps=T, widths=widths, rng_state=99001, record_distrib=True,
+                 record_last_step=True)
     tr.set_params(POLICY, init_policy(D, *widths, seed=71))
     tr.set_params(VALUE, init_value(B, D, seed=72))
     tr.rollout()

@@ -212,7 +212,7 @@ def test_weights20_logits(ctx):
                                                 POLICY)
     g = golden("deep_w20")
     tr = Trainer(ctx, algo="ppo", bins=8, dims=2, num_envs=64, steps=1,
-                 widths=(128, 64))
+                 widths=(128, 64), record_last_step=True)
     tr.set_params(POLICY, g["params"])
     obs = g["obs"].reshape(64, 8, 4)
     bins = np.zeros((2, 64, 8, 2), np.int8)

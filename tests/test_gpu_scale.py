@@ -3,7 +3,8 @@ size-independent properties at the full BASELINE config-3 size."""
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_grad_close, assert_grad_units
+from conftest import (assert_close, assert_grad_close, assert_grad_units,
+                      log_record)
 
 pytestmark = pytest.mark.gpu
 
@@ -108,7 +109,7 @@ def test_c3_full_size_properties(ctx):
 
     def make():
         tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
-                     rng_state=20241008)
+                     rng_state=20241008, record_last_step=True)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         return tr
@@ -189,7 +190,7 @@ def test_wave_rollout_matches_4wave(ctx, monkeypatch, algo, N, B, D, T):
         # bf16-split one: test_split_rollout_matches_f32)
         monkeypatch.setenv("XH_ROLLOUT_KERNEL", "4" if kern == "4" else "f32")
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
-                     widths=(128, 128), rng_state=99)
+                     widths=(128, 128), rng_state=99, record_last_step=True)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         tr.rollout()
@@ -292,7 +293,7 @@ def _c3_health_run(ctx, iters, **kw):
     from dependence_free_rl_amd.trainer import BUF_ADV
     N, B, D, T = 32768, 64, 2, 4
     tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
-                 rng_state=20241008, **kw)
+                 rng_state=20241008, record_last_step=True, **kw)
     tr.set_params(POLICY, init_policy(D, 128, 128, seed=0))
     tr.set_params(VALUE, init_value(B, D, seed=1))
     log = []
@@ -411,7 +412,7 @@ def test_split_rollout_matches_f32(ctx, monkeypatch, algo, N, B, D, T):
         else:
             monkeypatch.delenv("XH_ROLLOUT_KERNEL", raising=False)
         tr = Trainer(ctx, algo=algo, bins=B, dims=D, num_envs=N, steps=T,
-                     widths=H, rng_state=77)
+                     widths=H, rng_state=77, record_last_step=True)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         if forced is not None:
@@ -429,7 +430,13 @@ def test_split_rollout_matches_f32(ctx, monkeypatch, algo, N, B, D, T):
     for b in (BUF_LOGITS, BUF_PROBS, BUF_POLD):
         np.testing.assert_allclose(forced[b], ref[b], rtol=2e-5, atol=1e-7,
                                    err_msg="buffer %d" % b)
-    mism = int((free[BUF_ACTION] != ref[BUF_ACTION]).sum())
-    print("free-running split vs f32 rollout: %d of %d actions differ" % (
-        mism, ref[BUF_ACTION].size))
+    diff = free[BUF_ACTION] != ref[BUF_ACTION]
+    mism = int(diff.sum())
+    envs = int(diff.any(0).sum())  # an env diverges from its first mismatch on
+    print("free-running split vs f32 rollout: %d of %d actions differ (%d envs)"
+          % (mism, ref[BUF_ACTION].size, envs))
+    log_record("sampling_agreement.jsonl", {
+        "test": "split_vs_f32_rollout", "algo": algo, "N": N, "B": B, "D": D,
+        "T": T, "actions": int(ref[BUF_ACTION].size), "differ": mism,
+        "envs_differ": envs})
     assert mism <= 1e-4 * ref[BUF_ACTION].size

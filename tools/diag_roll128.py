@@ -17,7 +17,7 @@ for N in (4104, 8192, 16384):
         else:
             os.environ.pop("XH_ROLLOUT_KERNEL", None)
         tr = Trainer(ctx, algo="ac", bins=B, dims=D, num_envs=N, steps=T,
-                     widths=(128, 128), rng_state=99)
+                     widths=(128, 128), rng_state=99, record_last_step=True)
         tr.set_params(POLICY, pp)
         tr.set_params(VALUE, vp)
         tr.rollout()

@@ -10,9 +10,16 @@ loads; tools/probes/fetch_probe.hip measured the same 1/2 for 1-, 2-, 4- and
 16-byte lanes: 1 GiB read -> 524298 KB, profiles/r03_probe_fetch_write.txt),
 WRITE_SIZE the bytes written (256 MiB of 4-byte stores -> 262144 KB), so
 hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE; the raw read figure is kept too.
+
+The summary's "_meta" entry ties it to the build it profiled: the sha256 of
+the libxylo_hip.so in this tree (the library the profiled bench loaded), the
+tag and the creation time.  bench.py cites a summary's traffic only when its
+library_sha256 equals the sha256 of the library the bench itself loaded.
 """
 import collections
 import csv
+import datetime
+import hashlib
 import glob
 import json
 import os
@@ -46,6 +53,18 @@ def per_kernel_all(path):
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 
+def library_sha256(repo):
+    """sha256 of the product library in `repo` (XH_LIB_PATH when set: the
+    library the profiled process loaded)."""
+    path = os.environ.get("XH_LIB_PATH") or os.path.join(
+        repo, "dependence_free_rl_amd", "libxylo_hip.so")
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def main(tag, trace, fetch, write, *sq_dirs):
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.environ.get("PROFILE_OUT", os.path.join(here, "profiles"))
@@ -76,6 +95,11 @@ def main(tag, trace, fetch, write, *sq_dirs):
             e["clock_ghz"] = g / 8.0 / ns
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in sq:
             e["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 1024)
+    summary["_meta"] = {
+        "tag": tag,
+        "library_sha256": library_sha256(here),
+        "created": datetime.datetime.now(datetime.timezone.utc).isoformat(
+            timespec="seconds")}
     with open(os.path.join(out, "%s_pmc_summary.json" % tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps({k: v for k, v in summary.items() if "policy_train" in k},
