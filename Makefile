@@ -16,8 +16,9 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \
             $(SRC)/policy_split4h_kernels.o $(SRC)/policy_split4h_kl_kernels.o \
-            $(SRC)/loss_kernels.o \
-            $(SRC)/train_select.o $(SRC)/model_api.o $(SRC)/xylo_hip.o
+            $(SRC)/loss_kernels.o $(SRC)/tensor_kernels.o \
+            $(SRC)/train_select.o $(SRC)/model_api.o $(SRC)/tensor_api.o \
+            $(SRC)/xylo_hip.o
 # superseded train kernels (the config-3 / config-5
 # epoch's earlier forms), kept for A/B runs in the variant library only
 VARIANT_KERNELS := policy_split_kernels policy_split128_kernels \
@@ -84,6 +85,9 @@ $(SRC)/train_select.o: $(SRC)/train_select.cpp $(HDRS)
 $(SRC)/model_api.o: $(SRC)/model_api.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(SRC)/tensor_api.o: $(SRC)/tensor_api.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 # the variant library: the product objects + the superseded train kernels,
 # with the dispatch that reaches them (XH_TRAIN_KERNEL=split4w / split8w /
 # split8wp / split4p / split8wg / split128); loaded through XH_LIB_PATH only
@@ -120,7 +124,8 @@ oracle:
 # test programs of the drop-in layer (tests/compat), prebuilt so the GPU box
 # runs them without a compiler step
 COMPAT_TESTS := $(COMPAT)/bound_env_by_hand $(COMPAT)/save_weights \
-                $(COMPAT)/composed_learner
+                $(COMPAT)/composed_learner $(COMPAT)/tensor_ops \
+                $(COMPAT)/tensor_device
 
 compat: $(EXAMPLES) $(COMPAT_TESTS)
 	@mkdir -p $(COMPAT)
@@ -141,6 +146,22 @@ $(COMPAT)/save_weights: tests/compat/save_weights.cc $(COMPAT_HDRS) $(LIB)
 $(COMPAT)/composed_learner: tests/compat/composed_learner.cc $(COMPAT_HDRS) $(LIB)
 	@mkdir -p $(COMPAT)
 	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
+
+$(COMPAT)/tensor_ops: tests/compat/tensor_ops.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
+
+$(COMPAT)/tensor_device: tests/compat/tensor_device.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) $< $(LDCOMPAT) -o $@
+
+# the host paths of the drop-in tensor layer under AddressSanitizer +
+# UndefinedBehaviorSanitizer (tests/test_tensor_compat.py runs it
+# with every operation kept on the host)
+$(COMPAT)/tensor_ops_asan: tests/compat/tensor_ops.cc $(COMPAT_HDRS) $(LIB)
+	@mkdir -p $(COMPAT)
+	$(CXX20) $(CXXFLAGS20) -O1 -g -fsanitize=address,undefined \
+	    -fno-omit-frame-pointer -fno-sanitize-recover=undefined $< $(LDCOMPAT) -o $@
 
 $(COMPAT)/%: examples/%.cc $(COMPAT_HDRS) $(LIB)
 	@mkdir -p $(COMPAT)

@@ -993,4 +993,15 @@ hipError_t layer_gradient(const ModelLayer &L, const float *x, int rows,
   return launch_slab_reduce(slab, splits, stride, L.out * L.in + L.out, grad, s);
 }
 
+// xylo::matmul_transposed / matmul (tensor.cc:218-230) on device arrays
+hipError_t launch_tensor_gemm(bool b_nk, const float *A, const float *B,
+                              float *C, int M, int N, int K, hipStream_t st) {
+  using namespace dense;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const RowMajor la{A, K};
+  const EpStore ep{C, N};
+  if (b_nk) return gemm(la, RowMajor{B, K}, ep, M, N, K, nullptr, 0, 1, st);
+  return gemm(la, ColMajor{B, N}, ep, M, N, K, nullptr, 0, 1, st);
+}
+
 }  // namespace xh

@@ -436,4 +436,35 @@ hipError_t launch_slab_reduce_opt(const float *slab, int nslab, int stride,
                                   float *v, OptStep o, hipStream_t s,
                                   SlabAlias al = SlabAlias{0, 0, 0, 0});
 
+
+// xylo/tensor.{h,cc} arithmetic on device arrays (tensor_kernels.hip; the
+// drop-in tensor type's device tensors and large host operations).
+enum TensorMapOp {
+  kTensorAdd = 0, kTensorMinus = 1, kTensorMultiply = 2, kTensorDivide = 3,
+  kTensorAddS = 4, kTensorMinusS = 5, kTensorMultiplyS = 6, kTensorDivideS = 7,
+  kTensorAbs = 8, kTensorSin = 9, kTensorExp = 10, kTensorLog = 11,
+  kTensorSqrt = 12, kTensorFill = 13, kTensorRMinusS = 14, kTensorRDivideS = 15
+};
+enum TensorReduceOp {
+  kTensorSum = 0, kTensorDot = 1, kTensorSqDev = 2, kTensorMax = 3,
+  kTensorArgmax = 4
+};
+// out[i] = op(a[i], b[i], s) for i < n (b: the binary ops; s: the scalar ops
+// and fill)
+hipError_t launch_tensor_map(int op, const float *a, const float *b, float s,
+                             float *out, long n, hipStream_t st);
+// workgroup partials of a reduction over n elements; scratch holds
+// tensor_reduce_parts(n) + 1 records of 16 bytes, the result (double value,
+// int64 index) in the last
+int tensor_reduce_parts(long n);
+hipError_t launch_tensor_reduce(int op, const float *a, const float *b, float s,
+                                long n, void *scratch, hipStream_t st);
+hipError_t launch_tensor_transpose(const float *in, float *out, int rows,
+                                   int cols, hipStream_t st);
+// C[m][n] = sum_k A[m][k] B(n, k): b_nk = B is [N][K] (matmul_transposed,
+// tensor.cc:218-227), else B is [K][N] (matmul, :228-230); the Dense f32-MFMA
+// GEMM (dense_kernels.hip)
+hipError_t launch_tensor_gemm(bool b_nk, const float *A, const float *B,
+                              float *C, int M, int N, int K, hipStream_t st);
+
 }  // namespace xh

@@ -38,24 +38,6 @@
 
 namespace xylo {
 
-namespace detail {
-// The process-wide device context (XYLO_HIP_DEVICE picks the GPU).
-inline xh_ctx *hip_context() {
-  struct holder {
-    xh_ctx *h = nullptr;
-    holder() {
-      const char *d = std::getenv("XYLO_HIP_DEVICE");
-      if (xh_ctx_create(d ? std::atoi(d) : 0, 0, 1, nullptr, &h) != XH_OK)
-        throw xeno::error(std::string("xylo-hip: xh_ctx_create: ") +
-                          xh_last_error());
-    }
-    ~holder() { xh_ctx_destroy(h); }
-  };
-  static holder c;
-  return c.h;
-}
-}  // namespace detail
-
 inline void normal_initialize(std::size_t, vector_view v) {
   normal_distribution(0, 0.01, v);
 }
@@ -69,10 +51,6 @@ inline void he_initialize(std::size_t fan_in, vector_view v) {
 enum class layer_kind { full, conv1d_1, relu, softmax, softmax_xent, custom };
 
 namespace detail {
-inline void hip_check(int status, const char *what) {
-  if (status != XH_OK)
-    throw xeno::error(std::string("xylo-hip: ") + what + ": " + xh_last_error());
-}
 // a non-null pointer for empty parameter arrays (the ABI rejects null)
 inline float *nonnull(float *p) {
   static float dummy = 0.0f;
@@ -169,7 +147,9 @@ class convolution1d_1_layer : public detail::dense_base {
 class activation_layer : public layer {
  public:
   explicit activation_layer(std::string_view name = "") : layer(name) {}
-  vector_view parameters() const override { return {}; }
+  vector_view parameters() const override {
+    return vector_view(nullptr, std::size_t(0));
+  }
 };
 
 class relu_activation : public activation_layer {
@@ -182,7 +162,9 @@ class relu_activation : public activation_layer {
 class softmax_layer : public layer {
  public:
   explicit softmax_layer(std::string_view name = "") : layer(name) {}
-  vector_view parameters() const override { return {}; }
+  vector_view parameters() const override {
+    return vector_view(nullptr, std::size_t(0));
+  }
   layer_kind kind() const override { return layer_kind::softmax; }
 };
 
@@ -617,8 +599,11 @@ class momentum_optimizer : public optimizer {
  protected:
   vector next_parameters(const vector &parameters, const vector &gradient,
                          float rate) override {
-    if (velocity_.size() != parameters.size())
-      velocity_ = vector({parameters.size()});  // zeros, on first use
+    if (velocity_.size() != parameters.size()) {  // zeros, on first use
+      vector z({parameters.size()});
+      z = 0.0f;
+      velocity_.swap(z);
+    }
     return device_update(XH_OPT_MOMENTUM, parameters, gradient, rate, 0.0f,
                          0.9f, 0.0f, 1.0f, &velocity_, nullptr);
   }
@@ -640,8 +625,11 @@ class adam_optimizer : public optimizer {
   vector next_parameters(const vector &parameters, const vector &gradient,
                          float rate) override {
     if (first_moment_.size() != parameters.size()) {
-      first_moment_ = vector({parameters.size()});
-      second_moment_ = vector({parameters.size()});
+      vector z1({parameters.size()}), z2({parameters.size()});
+      z1 = 0.0f;
+      z2 = 0.0f;
+      first_moment_.swap(z1);
+      second_moment_.swap(z2);
     }
     vector p = device_update(XH_OPT_ADAM, parameters, gradient, rate, 0.0f,
                              beta1_, beta2_, t_, &first_moment_,

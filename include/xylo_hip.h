@@ -443,6 +443,58 @@ int xh_optimizer_apply(xh_ctx *ctx, int kind, float lr, float weight_decay,
  * batch): the batch's final states become the next rollout's start states. */
 int xh_trainer_forget(xh_trainer *t);
 
+/* ---------------------------------------------------------- tensor ---- */
+/* xylo/tensor.{h,cc} on the device, for the drop-in tensor type
+ * (include/xylo_compat/xylo/tensor.h): tensors created with on_device = true
+ * live in HBM (the reference's memory_blob on_device bit with its gpu_alloc /
+ * gpu_dealloc stubs, tensor.cc:38-39, 78-102, made real), and their
+ * arithmetic runs here; large operations on host tensors (GEMMs, long
+ * reductions) stage through the device.  Every call is synchronous on the
+ * context's stream.
+ *
+ * xh_tensor_alloc / free: n floats of device memory, zero-filled (NULL for
+ * n = 0).
+ * xh_tensor_copy: n floats, kind XH_COPY_H2D | XH_COPY_D2H | XH_COPY_D2D. */
+enum { XH_COPY_H2D = 0, XH_COPY_D2H = 1, XH_COPY_D2D = 2 };
+int xh_tensor_alloc(xh_ctx *ctx, size_t n, float **out);
+int xh_tensor_free(xh_ctx *ctx, float *p);
+int xh_tensor_copy(xh_ctx *ctx, float *dst, const float *src, size_t n,
+                   int kind);
+/* Elementwise, device arrays (tensor.cc:256-317 and the compound operators
+ * :338-398): out[i] = a[i] + b[i] | a - b | a * b | a / b (XH_T_ADD ..
+ * XH_T_DIVIDE); a[i] + s | a - s | a * s | a / s (XH_T_*_S); fabsf / sinf /
+ * expf / logf / sqrtf of a[i]; XH_T_FILL: out[i] = s (vector::operator=(float),
+ * tensor.cc:128); XH_T_RMINUS_S s - a[i] and XH_T_RDIVIDE_S s / a[i] (the
+ * reference's compound v -= s and v /= s, whose bind_front puts the scalar
+ * first: tensor.cc:378-380, 392-394).  out may alias a or b. */
+enum { XH_T_ADD = 0, XH_T_MINUS = 1, XH_T_MULTIPLY = 2, XH_T_DIVIDE = 3,
+       XH_T_ADD_S = 4, XH_T_MINUS_S = 5, XH_T_MULTIPLY_S = 6,
+       XH_T_DIVIDE_S = 7, XH_T_ABS = 8, XH_T_SIN = 9, XH_T_EXP = 10,
+       XH_T_LOG = 11, XH_T_SQRT = 12, XH_T_FILL = 13, XH_T_RMINUS_S = 14,
+       XH_T_RDIVIDE_S = 15 };
+int xh_tensor_map(xh_ctx *ctx, int op, const float *a, const float *b,
+                  float scalar, float *out, size_t n);
+/* Reductions over n floats (device arrays if on_device, else host arrays
+ * staged for the call), accumulated in double and returned unrounded:
+ * XH_R_SUM sum a (tensor.cc:434-438), XH_R_DOT sum a*b (:427-432), XH_R_SQDEV
+ * sum (a - s)^2 (variance's sum about the mean s, :442-451), XH_R_MAX max a
+ * (:462), XH_R_ARGMAX its first index (:464-466) in *index (may be NULL
+ * otherwise).  max / argmax of n = 0 is XH_ERR_INVALID. */
+enum { XH_R_SUM = 0, XH_R_DOT = 1, XH_R_SQDEV = 2, XH_R_MAX = 3,
+       XH_R_ARGMAX = 4 };
+int xh_tensor_reduce(xh_ctx *ctx, int op, const float *a, const float *b,
+                     float scalar, size_t n, int on_device, double *value,
+                     int64_t *index);
+/* out[m][n] = sum_k a[m][k] b(n, k), f32 MFMA: XH_GEMM_NT b is [n][k]
+ * (matmul_transposed, tensor.cc:218-227), XH_GEMM_NN b is [k][n] (matmul,
+ * :228-230).  Row-major, no aliasing of out with a or b. */
+enum { XH_GEMM_NT = 0, XH_GEMM_NN = 1 };
+int xh_tensor_gemm(xh_ctx *ctx, int layout, const float *a, const float *b,
+                   float *out, int m, int n, int k, int on_device);
+/* out[cols][rows] = in[rows][cols]^T (transpose, tensor.cc:209-216). */
+int xh_tensor_transpose(xh_ctx *ctx, const float *in, float *out, int rows,
+                        int cols, int on_device);
+
 /* sizeof of the ABI structs ("xh_config", "xh_eval", "xh_layer"; 0 if
  * unknown), so a
  * foreign-language binding can check its mirror of them. */

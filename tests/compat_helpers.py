@@ -53,3 +53,58 @@ def read_rounds(cmd, n, env, cwd=None, timeout=300):
 def fmt6(x):
     """std::ostream's default float formatting (precision 6, %g)."""
     return float("%g" % x)
+
+
+# ------------------------------------------------ xylo/tensor.h fixtures --
+def parse_tensor_ops(text):
+    """{name: value} of tests/compat/tensor_ops.cc's output: float32 / int64
+    arrays, or strings."""
+    import numpy as np
+    out = {}
+    for line in text.splitlines():
+        if not line.strip():
+            continue
+        name, kind, rest = line.split(" ", 2)
+        if kind == "s":
+            out[name] = rest
+            continue
+        parts = rest.split()
+        n, vals = int(parts[0]), parts[1:]
+        assert len(vals) == n, (name, n, len(vals))
+        out[name] = (np.array([float(v) for v in vals], np.float32) if kind == "f"
+                     else np.array([int(v) for v in vals], np.int64))
+    return out
+
+
+def tensor_ops_mismatches(text, tol=1e-4):
+    """tensor_ops output against tests/golden/tensor_ops.npz (the reference's
+    own build of the same source): integers (shapes, indices, flags, engine
+    draws) and strings bit-exact, floats within tol * max(1, |y|).  Returns
+    [(name, detail)] of the mismatches and the worst float error."""
+    import numpy as np
+    g = np.load(os.path.join(REPO, "tests", "golden", "tensor_ops.npz"))
+    kinds = dict(k.split(":") for k in g["__kinds"])
+    got = parse_tensor_ops(text)
+    bad = [(k, "missing") for k in kinds if k not in got]
+    bad += [(k, "unexpected") for k in got if k not in kinds]
+    worst = 0.0
+    for k, kind in kinds.items():
+        if k not in got:
+            continue
+        y, x = g[k], got[k]
+        if kind == "s":
+            if str(y) != x:
+                bad.append((k, "%r != %r" % (x, str(y))))
+        elif kind == "i":
+            if not np.array_equal(x, y):
+                bad.append((k, "ints differ"))
+        else:
+            if x.shape != y.shape:
+                bad.append((k, "shape %s != %s" % (x.shape, y.shape)))
+                continue
+            err = np.abs(x.astype(np.float64) - y) / np.maximum(1.0, np.abs(y))
+            e = float(err.max()) if err.size else 0.0
+            worst = max(worst, e)
+            if not e <= tol:
+                bad.append((k, "err %.3g" % e))
+    return bad, worst
