@@ -335,6 +335,9 @@ void *buffer_ptr(const xh_trainer *t, int which) {
 }
 
 constexpr uint64_t kEvalStride = 1ull << 26;  // draws between env streams
+// row groups one policy-train workgroup sums into its gradient slab at most
+// (= BASELINE configs 3 and 5 per GPU: 131072 groups over 256 workgroups)
+constexpr int kMaxTrainDepth = 512;
 constexpr int kBinCapacity = 8;             // bin_packing.h:48, every dim
 
 xh::EnvDesc make_env(int bins, int dims) {
@@ -1485,8 +1488,19 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     t->pslab_n = xh::policy_train_grid(c.bins, c.dims, c.policy_h1, c.policy_h2,
                                        c.algo == XH_KLPPO);
     const int groups = (int)(T * N / (size_t)G);
-    if (c.train_grid_cap > 0 && t->pslab_n > c.train_grid_cap)
-      t->pslab_n = c.train_grid_cap;  // test-only depth control (xylo_hip.h)
+    if (c.train_grid_cap > 0) {
+      if (t->pslab_n > c.train_grid_cap)
+        t->pslab_n = c.train_grid_cap;  // test-only depth control (xylo_hip.h)
+    } else if (groups > t->pslab_n * kMaxTrainDepth) {
+      // a batch beyond one GPU's BASELINE share (the 8-GPU jobs' whole
+      // batches on one device): more workgroups than the one-per-CU grid, so
+      // that no f32 gradient slab accumulates more than kMaxTrainDepth row
+      // groups -- the depth the bench configurations run at, where the
+      // tests hold the gradient error flat (tests/test_gpu_depth.py).  A
+      // multiple of 8 keeps the kernels' XCD-aware work order.
+      const int want = (groups + kMaxTrainDepth - 1) / kMaxTrainDepth;
+      t->pslab_n = (want + 7) & ~7;
+    }
     if (t->pslab_n > groups) t->pslab_n = groups;
     t->pslab_stride = (t->np + 63) & ~63;
     t->vslab_n = 256;

@@ -80,6 +80,17 @@ def test_global_workload_8_ranks(ctx, cfg):
 
     full = make(Ng, 0)
     ranks = [make(n, r * n) for r in range(W)]
+    # the 8n-env batch trains on 8x the workgroups of one rank, so that no
+    # gradient slab sums more row groups than a rank's (the bench depth);
+    # at 4096 groups per slab the f32 sums of the full batch drifted 2e-2
+    # (relative L2) from the ranks' (profiles/r05a_global_sums.jsonl)
+    for tr in [full] + ranks:
+        tr.rollout()
+        tr.learn()
+    grid = [tr.kernel_info()["train_grid"] for tr in [full] + ranks]
+    assert grid[0] == W * grid[1] and len(set(grid[1:])) == 1, grid
+    full = make(Ng, 0)
+    ranks = [make(n, r * n) for r in range(W)]
     for it in range(2):
         for tr in [full] + ranks:
             tr.rollout()
