@@ -1,6 +1,6 @@
 // policy_split8wh_kernels.hip -- the PPO / actor-critic train epoch of the
 // 64-bin 2-D [128,128] policy (BASELINE configs 3 and 4): the pipelined
-// 8-wave kernel of policy_split8wp_kernels.hip with layer 2 and dH1 on the
+// 8-wave kernel of variants/policy_split8wp_kernels.hip with layer 2 and dH1 on the
 // f16 matrix cores, each f32 operand scaled by a power of two and split
 // EXACTLY into two f16 parts ("f16 pairs"):
 //
@@ -23,7 +23,7 @@
 // dW2's operand g (x) H1 has no bound known before the kernel (g ~ A / p_old),
 // so dW2 keeps the exact three-part bf16 split.  MFMAs per wave per 64-row
 // group: 192 -> 128.  Pipeline, layouts and swizzles as in
-// policy_split8wp_kernels.hip:
+// variants/policy_split8wp_kernels.hip:
 //
 // Why: the two waves of a SIMD run the same phases in lockstep, so a VALU
 // block and an MFMA block do not overlap, while VALU instructions issued

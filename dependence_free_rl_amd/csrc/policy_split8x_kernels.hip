@@ -21,7 +21,7 @@
 // Three units' pre-activations are live (v: its masks in X(v); v+1 waiting;
 // v+2 accumulating).  Wave 0 stages unit v+3 during X(v): its 64 rows' bins
 // and its env's record (action 0..127, old probability, advantage, item).
-// Layouts, swizzles and operand maps as policy_split8wp_kernels.hip.
+// Layouts, swizzles and operand maps as variants/policy_split8wp_kernels.hip.
 #include <cstdlib>
 
 #include "xh_device.h"

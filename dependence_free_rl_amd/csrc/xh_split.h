@@ -259,8 +259,8 @@ __device__ __forceinline__ void img_store_h2(char *img_hi, char *img_lo, int bas
   }
 }
 
-// ---- helpers of the split train kernels (policy_split_kernels.hip,
-// policy_split128_kernels.hip)
+// ---- helpers of the split train kernels (variants/policy_split_kernels.hip,
+// variants/policy_split128_kernels.hip)
 namespace split {
 
 __device__ __forceinline__ float relu(float x) {
