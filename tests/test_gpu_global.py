@@ -34,10 +34,11 @@ pytestmark = pytest.mark.gpu
 M31, A = 2147483647, 16807
 
 # (relative L2, worst entry / max |g|) of the 8-rank sum against the 8n-env
-# gradient, fp32 sums over 8n * T * B rows in two orders.  About 3x the
-# values measured on the first run (logged to gpurun_out/global_sums.jsonl,
-# copied to profiles/r05*_global_sums.jsonl).
-GLOBAL_SUM_LIMITS = {64: (2e-3, 6e-3), 128: (8e-3, 3e-2)}
+# gradient, fp32 sums over 8n * T * B rows in two orders at the same slab
+# depth.  About 3x the values measured (policy gradient, the larger of the two
+# iterations; profiles/r05b_global_sums.jsonl: config 4 9.0e-5 / 1.8e-4,
+# config 5 1.1e-4 / 2.2e-4; the value gradients agree to 2e-6)
+GLOBAL_SUM_LIMITS = {64: (3e-4, 6e-4), 128: (4e-4, 7e-4)}
 
 
 def _positions(x0, base, step, n):
