@@ -13,6 +13,7 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o \
+            $(SRC)/policy_spec8_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \
             $(SRC)/policy_split4h_kernels.o $(SRC)/policy_split4h_kl_kernels.o \
@@ -25,6 +26,7 @@ VARIANT_KERNELS := policy_split_kernels policy_split128_kernels \
             policy_split8w_kernels policy_split8wp_kernels \
             policy_split4p_kernels policy_split8wg_kernels
 HDRS     := $(SRC)/xh_device.h $(SRC)/xh_kernels.h $(SRC)/xh_split.h \
+            $(SRC)/spec8_layout.h \
             $(SRC)/xh_host.h include/xylo_hip.h
 
 # Drop-in C++20 layer (include/xylo_compat): the reference's unmodified
@@ -59,6 +61,7 @@ FLAGS_policy_split8wh_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split8x_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split4h_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split8wg_kernels := -mllvm -amdgpu-mfma-vgpr-form
+FLAGS_policy_spec8_kernels := -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@

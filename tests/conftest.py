@@ -89,7 +89,7 @@ def assert_grad_close(x, y, mag, n_terms, sides=1, what=""):
 # the tests), so the comparison measures one epoch's arithmetic, not the two
 # trajectories' drift.
 # the train kernel the 64-bin 2-D [128,128] shape runs by default
-HEADLINE_TRAIN_KERNEL = "policy_train_split8wh_kernel"
+HEADLINE_TRAIN_KERNEL = "policy_train_spec8_kernel"
 
 GRAD_UNITS_MEDIAN = 1.0
 GRAD_UNITS_P99 = 100.0

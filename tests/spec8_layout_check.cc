@@ -1,0 +1,140 @@
+// Exhaustive host check of the spec8 train kernel's LDS image layout
+// (dependence_free_rl_amd/csrc/spec8_layout.h), run by
+// tests/test_spec8_layout.py:
+//   * poff is a bijection of each image onto its bytes;
+//   * every lane base + loop immediate the kernel uses addresses the element
+//     the MFMA operand map / C layout asks for;
+//   * bank conflicts per access pattern by the lane groups and bank rules of
+//     MI355X_MICROARCH.md §LDS (stores 2-way, reads conflict-free).
+// Prints one line per check and exits non-zero on the first failure.
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "spec8_layout.h"
+
+using namespace xh::sp8;
+
+static int fails = 0;
+#define CHECK(c, ...)              \
+  do {                             \
+    if (!(c)) {                    \
+      std::printf("FAIL: ");       \
+      std::printf(__VA_ARGS__);    \
+      std::printf("\n");           \
+      ++fails;                     \
+      if (fails > 20) std::exit(1); \
+    }                              \
+  } while (0)
+
+// worst bank multiplicity of one instruction: groups of lanes, each lane
+// touching `dwords` consecutive dwords from its byte address
+static int ways(const std::vector<std::vector<int>> &groups, const int *addr, int dwords,
+                int banks) {
+  int worst = 1;
+  for (const auto &g : groups) {
+    std::map<int, std::set<int>> per_bank;  // bank -> distinct dword addresses
+    for (int l : g)
+      for (int d = 0; d < dwords; ++d) {
+        const int dw = addr[l] / 4 + d;
+        per_bank[dw % banks].insert(dw);
+      }
+    for (auto &kv : per_bank) worst = std::max(worst, (int)kv.second.size());
+  }
+  return worst;
+}
+
+static std::vector<std::vector<int>> contiguous(int n) {
+  std::vector<std::vector<int>> g(64 / n);
+  for (int l = 0; l < 64; ++l) g[l / n].push_back(l);
+  return g;
+}
+
+static std::vector<std::vector<int>> b128_groups() {
+  auto add = [](std::vector<int> &v, int a, int b) {
+    for (int l = a; l <= b; ++l) v.push_back(l);
+  };
+  std::vector<std::vector<int>> g(4);
+  add(g[0], 0, 3), add(g[0], 12, 15), add(g[0], 20, 27);
+  add(g[1], 4, 11), add(g[1], 16, 19), add(g[1], 28, 31);
+  add(g[2], 32, 35), add(g[2], 44, 47), add(g[2], 52, 59);
+  add(g[3], 36, 43), add(g[3], 48, 51), add(g[3], 60, 63);
+  return g;
+}
+
+int main() {
+  // bijection, both image shapes
+  for (int shape = 0; shape < 2; ++shape) {
+    const int X = shape == 0 ? 128 : 64, Y = shape == 0 ? 64 : 128, ny = Y / 32;
+    std::vector<int> seen(X * Y, 0);
+    for (int x = 0; x < X; ++x)
+      for (int y = 0; y < Y; ++y) {
+        const int o = poff(x, y, ny);
+        CHECK(o >= 0 && o < 2 * X * Y && o % 2 == 0, "poff range %d %d", x, y);
+        if (o >= 0 && o < 2 * X * Y) seen[o / 2]++;
+      }
+    for (int k = 0; k < X * Y; ++k) CHECK(seen[k] == 1, "poff not a bijection at %d", k);
+    std::printf("bijection [%d][%d]: ok\n", X, Y);
+  }
+  int addr[64];
+  int worst_store = 0, worst_row = 0, worst_tr = 0;
+  // stores from a C layout: lane row x = X0 + (l & 31), y = 32 T + 8 q + 4 h
+  for (int ny : {2, 4}) {
+    const int X = ny == 2 ? 128 : 64;
+    for (int X0 = 0; X0 < X; X0 += 32)
+      for (int T = 0; T < ny; ++T)
+        for (int q = 0; q < 4; ++q) {
+          for (int l = 0; l < 64; ++l) {
+            const int x = X0 + (l & 31), h = l >> 5, y = 32 * T + 8 * q + 4 * h;
+            addr[l] = wr_base(x, q, h, ny) + 1024 * T;
+            for (int u = 0; u < 4; ++u)
+              CHECK(addr[l] + 2 * u == poff(x, y + u, ny), "store ny%d x%d y%d", ny, x, y);
+            CHECK(addr[l] % 8 == 0, "store alignment");
+          }
+          worst_store = std::max(worst_store, ways(contiguous(16), addr, 2, 32));
+        }
+  }
+  // row reads: lane row x = X0 + (l & 31), y = 16 ks + 8 h .. +7
+  for (int ny : {2, 4}) {
+    const int X = ny == 2 ? 128 : 64;
+    for (int X0 = 0; X0 < X; X0 += 32)
+      for (int ks = 0; ks < 2 * ny; ++ks) {
+        for (int l = 0; l < 64; ++l) {
+          const int x = X0 + (l & 31), h = l >> 5, y = 16 * ks + 8 * h;
+          addr[l] = rd_base(x, ks & 1, h, ny) + 1024 * (ks >> 1);
+          for (int e = 0; e < 8; ++e)
+            CHECK(addr[l] + 2 * e == poff(x, y + e, ny), "row read ny%d x%d y%d", ny, x, y);
+          CHECK(addr[l] % 16 == 0, "row read alignment");
+        }
+        worst_row = std::max(worst_row, ways(b128_groups(), addr, 4, 64));
+      }
+  }
+  // transposed reads: k = x = 16 ks + 8 h + 4 n + j, column y = 32 T + (l & 31)
+  for (int ny : {2, 4}) {
+    const int X = ny == 2 ? 128 : 64;
+    for (int ks = 0; ks < X / 16; ++ks)
+      for (int T = 0; T < ny; ++T)
+        for (int n = 0; n < 2; ++n) {
+          for (int l = 0; l < 64; ++l) {
+            const int g = l >> 4, q = (l & 15) >> 2, p = l & 3, h = l >> 5;
+            const int x = 16 * ks + 8 * h + 4 * n + q, y = 32 * T + 16 * (g & 1) + 4 * p;
+            addr[l] = tr_base(l, n) + 1024 * (ks * ny + T);
+            for (int u = 0; u < 4; ++u)
+              CHECK(addr[l] + 2 * u == poff(x, y + u, ny), "tr read ny%d x%d y%d", ny, x, y);
+            CHECK(addr[l] % 8 == 0, "tr alignment");
+          }
+          // what each lane receives: column y of the 4 rows (the block's
+          // lane i gets column i): lane l, element j -> x = .. + j, y = 32 T + (l & 31)
+          worst_tr = std::max(worst_tr, ways(contiguous(32), addr, 2, 64));
+        }
+  }
+  std::printf("stores: %d-way\nrow reads: %d-way\ntransposed reads: %d-way\n", worst_store,
+              worst_row, worst_tr);
+  CHECK(worst_store <= 2, "stores %d-way", worst_store);
+  CHECK(worst_row == 1, "row reads %d-way", worst_row);
+  CHECK(worst_tr == 1, "transposed reads %d-way", worst_tr);
+  std::printf(fails ? "FAILED\n" : "ok\n");
+  return fails ? 1 : 0;
+}

@@ -35,7 +35,7 @@ DEPTH_CASES = [
     # config-2 shape: 1536 two-env groups; J = 3 (default grid 512), 16, 512, 1536
     ("c2", "ppo", 32, 1, (64, 64), 768, 4, (0, 96, 3, 1)),
 ]
-KERNELS = {64: "policy_train_split8wh_kernel", 128: "policy_train_split8x_kernel",
+KERNELS = {64: "policy_train_spec8_kernel", 128: "policy_train_split8x_kernel",
            32: "policy_train_split4h_kernel"}
 
 
