@@ -41,7 +41,7 @@
 // W2' pair 64, dH1 accumulators 32, two groups' H1 64).
 //
 // LDS (dynamic, base 0): g (x) H1 three bf16 parts [128 i][64 r] (48 KB), H1
-// two f16 parts [128 i][64 r] (32 KB), relu masks bf16 + f16 [64 r][128 o]
+// two f16 parts [64 r][128 i] (32 KB), relu masks bf16 + f16 [64 r][128 o]
 // in two slots (64 KB), then f32 vectors; image layout spec8_layout.h.
 #include <cstdlib>
 #include <type_traits>
@@ -70,6 +70,20 @@
 #ifndef XH_SP8_PRIO
 #define XH_SP8_PRIO 0
 #endif
+// XH_SP8_VBF (A/B builds): 0 lets the compiler schedule the vector waves'
+// phase-B blocks (dW1, layer 1) across block boundaries
+// XH_SP8_GH2 (A/B builds): 1 splits a block's two pairs in one MFMA slot
+// (two independent chains interleaved) and stores in the next
+#ifndef XH_SP8_GH2
+#define XH_SP8_GH2 0
+#endif
+#ifndef XH_SP8_VBF
+#define XH_SP8_VBF 0
+#endif
+#define VBFENCE()                                 \
+  do {                                            \
+    if (XH_SP8_VBF) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
 namespace xh {
 namespace sp8 {
 
@@ -278,7 +292,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // operand (g (x) H1 image, lane column i = 32 s + l31, row reads), the
     // mask stores from layer 2's C layout (lane row r = 32 t + l31, o = 32 s +
     // 8 q + 4 h ..; + 8192 t)
-    const int trH0 = opaque(tr_base(l, 0) + L_H1), trH1 = opaque(tr_base(l, 1) + L_H1);
+    // (layer 2's B operand: row reads of the [r][i] H1 image, lane row r =
+    // 32 t + l31, K-step ks: i = 16 ks + 8 h ..; + 8192 t + 1024 (ks >> 1))
+    const int rbH0 = opaque(rd_base(l31, 0, h, 4) + L_H1), rbH1 = opaque(rd_base(l31, 1, h, 4) + L_H1);
     const int trM0 = opaque(tr_base(l, 0) + L_MK), trM1 = opaque(tr_base(l, 1) + L_MK);
     const int rbg0 = rd_base(32 * s + l31, 0, h, 2) + L_GH,
               rbg1 = rd_base(32 * s + l31, 1, h, 2) + L_GH;
@@ -335,8 +351,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
 
     // layer 2 of the group in the H1 image: C[o][r] = S2 (b2 + W2 . H1) for
     // this wave's 32 o (registers) x r-tile t (lanes), 16 steps (t = st / 8,
-    // K-step ks = st % 8) of three f16 MFMAs; the B operand (H1 pair,
-    // transposed reads) one step ahead in ping-pong registers (the unrolled
+    // K-step ks = st % 8) of three f16 MFMAs; the B operand (H1 pair, row
+    // reads) one step ahead in ping-pong registers (the unrolled
     // step picks its buffer: no copies); task(k) after MFMA k
     auto layer2 = [&](f32x16s (&c)[2], auto &&task) {
 #pragma unroll
@@ -347,9 +363,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       }
       f16x8 bh[2], bl[2];
       auto ldB = [&](int st) {
-        const int o = 1024 * (2 * (st & 7) + (st >> 3));
-        bh[st & 1] = ldtrh(trH0 + o, trH1 + o);
-        bl[st & 1] = ldtrh(trH0 + o + kImg, trH1 + o + kImg);
+        const int t = st >> 3, ks = st & 7;
+        const int o = ((ks & 1) ? rbH1 : rbH0) + 8192 * t + 1024 * (ks >> 1);
+        bh[st & 1] = ld8h(o);
+        bl[st & 1] = ld8h(o + kImg);
       };
       ldB(0);
 #pragma unroll
@@ -716,21 +733,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       vwb[q] = opaque(wr_base(fi, q, h, 2) + L_GH);
-      vwH[q] = opaque(wr_base(fi, q, h, 2) + L_H1);
+      // the H1 image is [r][i]: lane row r = 32 t + l31 (+ 8192 t), values
+      // i = 32 v + 8 q + 4 h ..
+      vwH[q] = opaque(wr_base(l31, q, h, 4) + 1024 * v + L_H1);
     }
     const int rbm0 = opaque(rd_base(l31, 0, h, 4) + L_MK + kImg),
               rbm1 = opaque(rd_base(l31, 1, h, 4) + L_MK + kImg);
     float w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
 
     // S_H pre-activations of layer 1 of group gi (its bins in slot gi & 3)
-    // for this wave's features: two r-tiles of three bf16 MFMAs, C layout
-    // (lane column i, registers r = 32 t + 8 q + 4 h + u)
+    // for this wave's features: two r-tiles of three bf16 MFMAs with W1 as
+    // the A operand, C[i][r] (lane column r = 32 t + l31, registers i = 32 v
+    // + 8 q + 4 h + u): the [r][i] image's layout
     auto l1_mfma = [&](int gi, f32x16s (&pre)[2]) {
       const int sl = gi & 3;
       const bool ia =
           __builtin_amdgcn_readfirstlane(__float_as_int(lf[F_REC + 4 * sl + 3])) != 0;
-      // A fragment, lane row r = 32 t + l31, k = 8 h + e: (x0, x1), (1, ia),
-      // (ib, 0), (0, 0) in lane half 0, zeros in half 1
+      // X fragment (the B operand), lane column r = 32 t + l31, k = 8 h + e:
+      // (x0, x1), (1, ia), (ib, 0), (0, 0) in lane half 0, zeros in half 1
       const unsigned d1 = h ? 0u : (ia ? 0x3F803F80u : 0x00003F80u);
       const unsigned d2 = h ? 0u : (ia ? 0u : 0x00003F80u);
       const float *xv = lf + F_X + sl * 128 + l31;
@@ -739,10 +759,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
         const unsigned d0 = __builtin_bit_cast(
             unsigned, bf16x2{(__bf16)xv[32 * t], (__bf16)xv[64 + 32 * t]});
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const bf16x8 A = __builtin_bit_cast(bf16x8, u32x4{h ? 0u : d0, d1, d2, 0u});
-        pre[t] = mfma_bf16(A, w1p[2], f32x16s{});
-        pre[t] = mfma_bf16(A, w1p[1], pre[t]);
-        pre[t] = mfma_bf16(A, w1p[0], pre[t]);
+        const bf16x8 X = __builtin_bit_cast(bf16x8, u32x4{h ? 0u : d0, d1, d2, 0u});
+        pre[t] = mfma_bf16(w1p[2], X, f32x16s{});
+        pre[t] = mfma_bf16(w1p[1], X, pre[t]);
+        pre[t] = mfma_bf16(w1p[0], X, pre[t]);
       }
     };
     // B: layer 1 of group gi -> the H1 image (f16 pairs), block b = (t, q)
@@ -764,8 +784,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           hi[p] = __builtin_bit_cast(unsigned, y);
           lo[p] = __builtin_bit_cast(unsigned, z);
         }
-        st4h(vwH[q] + 1024 * t, __builtin_bit_cast(f16x4, u32x2{hi[0], hi[1]}));
-        st4h(vwH[q] + kImg + 1024 * t, __builtin_bit_cast(f16x4, u32x2{lo[0], lo[1]}));
+        st4h(vwH[q] + 8192 * t, __builtin_bit_cast(f16x4, u32x2{hi[0], hi[1]}));
+        st4h(vwH[q] + kImg + 8192 * t, __builtin_bit_cast(f16x4, u32x2{lo[0], lo[1]}));
       }
     };
     // x0, x1 -> three bf16 parts each, as bf16 pairs: v_cvt_pk_bf16_f32 and
@@ -831,9 +851,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           }
           case 1:
             split3_pair(x[0], x[1], ph[0], pm[0], pl[0]);
+            if (XH_SP8_GH2) split3_pair(x[2], x[3], ph[1], pm[1], pl[1]);
             break;
           case 2:
-            split3_pair(x[2], x[3], ph[1], pm[1], pl[1]);
+            if (!XH_SP8_GH2) split3_pair(x[2], x[3], ph[1], pm[1], pl[1]);
             break;
           default: {
             const int o2 = vwb[q] + 1024 * t;
@@ -880,7 +901,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       for (int b = 0; b < 8; ++b) {
         const int t = b >> 2, q = b & 3;
         if (b + 1 < 8) ld3(b + 1);
-        FENCE();
+        VBFENCE();
         const f32x4(&cur)[3] = gb[b & 1];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -889,7 +910,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           a1[u & 1] = fmaf(m, cur[2][u], a1[u & 1]);
           ag[u & 1] = fmaf(m, cur[0][u], ag[u & 1]);
         }
-        FENCE();
+        VBFENCE();
       }
       w0 += a0[0] + a0[1];
       w1 += a1[0] + a1[1];
