@@ -930,13 +930,15 @@ __global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) vo
 // discrete_distribution order, the exact restatement near a boundary) or the
 // forced action, and the env transition of slot t into slot t+1 -- one wave.
 // x: the env's minstd state (the caller loads / stores it); last: the
-// launch's last step (logits / probabilities outputs).  Out: nbv[k] = bin
-// k * 64 + lane in slot t+1, first = the next item is item_a.
+// launch's last step (logits / probabilities outputs).  In: nbv[k] = bin
+// k * 64 + lane of slot t and iv = slot t's item (the caller's registers: the
+// state is not read back from HBM); out: nbv[k] in slot t+1, first = the
+// next item is item_a.
 template <class S>
 __device__ __forceinline__ void sample_step128_x(const RolloutArgs &a, int t, bool last,
                                                  int env, const float (&z)[2],
                                                  uint32_t &x, int (&nbv)[2][S::D],
-                                                 bool &first) {
+                                                 const int (&iv)[S::D], bool &first) {
   const int lane = threadIdx.x & 63;
   const int N = a.b.N;
   float p[2];
@@ -992,20 +994,14 @@ __device__ __forceinline__ void sample_step128_x(const RolloutArgs &a, int t, bo
   }
   const float pold = choice < 64 ? wave_shfl(p[0], choice)
                                  : wave_shfl(p[1], choice - 64);
-  const size_t e = (size_t)t * N + env;
-  const int8_t *ip = a.b.items + e * 4;
-  int iv[S::D];
-#pragma unroll
-  for (int d = 0; d < S::D; ++d) iv[d] = ip[d];
   int nb[2][S::D];
   int neg[2] = {0, 0};
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int bin = k * 64 + lane;
-    const int8_t *bp = a.b.bins + e * S::BD + bin * S::D;
 #pragma unroll
     for (int d = 0; d < S::D; ++d) {
-      nb[k][d] = bin == choice ? bp[d] - iv[d] : bp[d];
+      nb[k][d] = bin == choice ? nbv[k][d] - iv[d] : nbv[k][d];
       neg[k] |= nb[k][d] < 0;
     }
   }
@@ -1039,9 +1035,17 @@ __device__ __forceinline__ void sample_step128(const RolloutArgs &a, int env,
                                                const float (&z)[2]) {
   const int lane = threadIdx.x & 63;
   uint32_t x = a.b.rng[env];
-  int nbv[2][S::D];
+  // slot a.t's bins of this lane and its item, from HBM
+  const size_t e = (size_t)a.t * a.b.N + env;
+  int nbv[2][S::D], iv[S::D];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int d = 0; d < S::D; ++d) nbv[k][d] = a.b.bins[e * S::BD + (k * 64 + lane) * S::D + d];
+#pragma unroll
+  for (int d = 0; d < S::D; ++d) iv[d] = a.b.items[e * 4 + d];
   bool first;
-  sample_step128_x<S>(a, a.t, true, env, z, x, nbv, first);
+  sample_step128_x<S>(a, a.t, true, env, z, x, nbv, iv, first);
   if (lane == 0) a.b.rng[env] = (a.t == a.b.T - 1) ? mstd_mulmod(x, a.jump_mul) : x;
 }
 
@@ -1284,7 +1288,7 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
           z[1] = zh;
       }
       bool first;
-      sample_step128_x<S>(a, t, t == t_last, env, z, x, own, first);
+      sample_step128_x<S>(a, t, t == t_last, env, z, x, own, it, first);
 #pragma unroll
       for (int d = 0; d < S::D; ++d) it[d] = first ? a.env.item_a[d] : a.env.item_b[d];
     }

@@ -80,6 +80,15 @@
 #ifndef XH_SP8_VBF
 #define XH_SP8_VBF 0
 #endif
+// XH_SP8_VAF (A/B builds): 0 lets the compiler schedule the vector waves'
+// phase-A slots (g (x) H1) across the dH1 MFMAs
+#ifndef XH_SP8_VAF
+#define XH_SP8_VAF 1
+#endif
+#define VAFENCE()                                 \
+  do {                                            \
+    if (XH_SP8_VAF) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
 #define VBFENCE()                                 \
   do {                                            \
     if (XH_SP8_VBF) __builtin_amdgcn_sched_barrier(0); \
@@ -869,18 +878,18 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       for (int st = 0; st < 16; ++st) {
         const int t = st >> 3, ks = st & 7, ca = st & 1;
         if (st + 1 < 16) ldA(st + 1);
-        FENCE();
+        VAFENCE();
         if (ks == 0)
           dh[t] = mfma_f16(A[ca], wd[ks][1], f32x16s{});
         else
           dh[t] = mfma_f16(A[ca], wd[ks][1], dh[t]);
-        FENCE();
+        VAFENCE();
         gh_slot(2 * st);
-        FENCE();
+        VAFENCE();
         dh[t] = mfma_f16(A[ca], wd[ks][0], dh[t]);
-        FENCE();
+        VAFENCE();
         gh_slot(2 * st + 1);
-        FENCE();
+        VAFENCE();
       }
     };
     // B(gi): dW1 / db1 / item sums of group gi: d = relu'(H1) dH1 g; sums
