@@ -12,7 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall \
 OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
-            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o \
+            $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/value_net_kernels.o \
             $(SRC)/policy_spec8_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \

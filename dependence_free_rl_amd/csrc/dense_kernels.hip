@@ -596,11 +596,25 @@ __global__ void reduce_w0_kernel(const float *W, int out, int B, int D,
   }
 }
 
-bool value_fused(const MlpArgs &a) {
+enum ValueKernel { kValGemm, kValMlp3, kValVnet };
+static ValueKernel value_kernel(const MlpArgs &a) {
   const char *e = std::getenv("XH_VALUE_KERNEL");
-  if (e && std::strcmp(e, "gemm") == 0) return false;
-  return a.nlayers == 3 && a.w[1] == dense::kFV1 && a.w[2] == dense::kFV2 &&
-         a.w[3] == 1;
+  if (e && std::strcmp(e, "gemm") == 0) return kValGemm;
+  const bool mlp3 = a.nlayers == 3 && a.w[1] == dense::kFV1 &&
+                    a.w[2] == dense::kFV2 && a.w[3] == 1;
+  if (!(e && std::strcmp(e, "mlp3") == 0) && vnet_shape_ok(a)) return kValVnet;
+  return mlp3 ? kValMlp3 : kValGemm;
+}
+static bool value_fused(const MlpArgs &a) { return value_kernel(a) == kValMlp3; }
+const char *value_kernel_name(const MlpArgs &a) {
+  switch (value_kernel(a)) {
+    case kValVnet: return "vnet_bf16";
+    case kValMlp3: return "mlp3_fused";
+    default: return "gemm";
+  }
+}
+bool value_reduced_slab(const MlpArgs &a) {
+  return value_kernel(a) == kValVnet || a.w0red != nullptr;
 }
 
 static hipError_t mlp3_forward(const MlpArgs &a, hipStream_t s) {
@@ -638,6 +652,7 @@ static hipError_t mlp3_forward(const MlpArgs &a, hipStream_t s) {
 
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s) {
   using namespace dense;
+  if (value_kernel(a) == kValVnet) return vnet_forward(a, s);
   if (value_fused(a)) return mlp3_forward(a, s);
   hipError_t e = hipSuccess;
   for (int l = 0; l < a.nlayers && e == hipSuccess; ++l) {
@@ -741,6 +756,8 @@ hipError_t value_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
                           float *targets, float *slab, int stride, int splits,
                           hipStream_t s) {
   using namespace dense;
+  if (value_kernel(a) == kValVnet)
+    return vnet_backward(a, va, gamma, targets, slab, stride, splits, s);
   if (!value_fused(a)) {
     ValueArgs v = va;
     v.row_g = a.grad[a.nlayers - 1];

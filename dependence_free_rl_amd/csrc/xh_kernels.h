@@ -204,6 +204,11 @@ struct MlpArgs {
   // their transition rows)
   float *v_term;
   const int *term_n;
+  // the bf16 value-net kernels (value_net_kernels.hip): scratch for W0's
+  // three-part fragments (vnet_frag_bytes), and the rows whose activations
+  // the forward stores for the backward (0: all, -1: none)
+  void *w0frag;
+  int act_rows;
 };
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s);
 // Weight gradients of every layer into slab[split] (flat layout), data
@@ -218,9 +223,21 @@ hipError_t mlp_backward(const MlpArgs &a, float *slab, int stride, int splits,
 hipError_t value_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
                           float *targets, float *slab, int stride, int splits,
                           hipStream_t s);
-// true: mlp_forward / value_backward run a fused (the Fin -> 64 -> 32 -> 1
-// shape, no XH_VALUE_KERNEL=gemm)
-bool value_fused(const MlpArgs &a);
+// The kernels mlp_forward / value_backward run for a value net:
+//   "vnet_bf16"  value_net_kernels.hip (Fin -> 64 -> 32 -> 1, B*D % 16 == 0,
+//                B*D + D < 416, w0frag set): the default
+//   "mlp3_fused" the f32 fused kernels (the same shape; XH_VALUE_KERNEL=mlp3)
+//   "gemm"       layer by layer (any shape; XH_VALUE_KERNEL=gemm)
+const char *value_kernel_name(const MlpArgs &a);
+// true: the value kernels write layer 0's gradient on the reduced
+// observation (bin 0's item columns only: slab_reduce needs SlabAlias)
+bool value_reduced_slab(const MlpArgs &a);
+bool vnet_shape_ok(const MlpArgs &a);
+size_t vnet_frag_bytes(const EnvDesc &e);
+hipError_t vnet_forward(const MlpArgs &a, hipStream_t s);
+hipError_t vnet_backward(const MlpArgs &a, const ValueArgs &va, float gamma,
+                         float *targets, float *slab, int stride, int splits,
+                         hipStream_t s);
 
 // model::eval of a described layer chain (dense_kernels.hip, xh_model_eval).
 enum LayerKind { kLayerFull = 0, kLayerConv1d = 1, kLayerRelu = 2,

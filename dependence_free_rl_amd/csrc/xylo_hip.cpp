@@ -80,6 +80,7 @@ struct xh_trainer {
   float *vgr[2] = {nullptr, nullptr};   // their dL/d(pre-activation)
   float *pslab = nullptr, *vslab = nullptr;
   float *vw0red = nullptr;  // value layer 0 on the reduced observation
+  uint8_t *vw0frag = nullptr;  // W0's bf16 fragments (value_net_kernels.hip)
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
   float *logits = nullptr, *probs = nullptr;
@@ -666,6 +667,7 @@ xh::MlpArgs value_mlp(xh_trainer *t, int rows, float *out) {
   // worth its extra launch from a 256-wide input on (config 2's 64-wide
   // layer 0 measured 1% slower with it)
   m.w0red = XH_VALUE_REDUCED && t->vl.Fin >= 256 ? t->vw0red : nullptr;
+  m.w0frag = t->vw0frag;
   return m;
 }
 
@@ -696,6 +698,7 @@ int do_learn(xh_trainer *t) {
   // transition rows (end rows have zero gradient), backward, one step
   // (the terminal views' values also land on their transition rows, v_term)
   xh::MlpArgs vm = value_mlp(t, NS + NT, t->v_state0);
+  vm.act_rows = NT;  // the backward reads the transition rows' activations
   vm.rows = t->vrows;
   vm.term_list = t->end_list;
   vm.v_term = t->v_term;
@@ -712,7 +715,7 @@ int do_learn(xh_trainer *t) {
   }));
   // the reduced layer 0 writes bin 0's item columns only (EpSlabRed)
   const xh::SlabAlias al =
-      vm.w0red ? xh::SlabAlias{t->cfg.value_h1, t->vl.Fin, t->cfg.bins,
+      xh::value_reduced_slab(vm) ? xh::SlabAlias{t->cfg.value_h1, t->vl.Fin, t->cfg.bins,
                                t->cfg.dims}
                : xh::SlabAlias{0, 0, 0, 0};
   CHK(reduce_and_step(t, XH_VALUE, t->vslab, t->vslab_n, t->vslab_stride,
@@ -721,6 +724,7 @@ int do_learn(xh_trainer *t) {
   // GAE zeroes V(terminal), the targets above used V(E_t)
   vm.max_rows = NS;
   vm.act[2] = t->v_state;
+  vm.act_rows = -1;  // no backward reads these
   CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
   va.v_state = t->v_state;
   va.row_g = nullptr;
@@ -1458,8 +1462,10 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     auto A = [&](auto **p, size_t bytes) {
       if (st == XH_OK) st = dalloc(t, p, bytes);
     };
-    A(&t->bins, (T + 1) * N * t->BD());
-    A(&t->items, (T + 1) * N * 4);
+    // + 64 B: the value forward's 8-byte loads may read past a row's last
+    // byte (vnet_forward_kernel; the bytes meet zero weights)
+    A(&t->bins, (T + 1) * N * t->BD() + 64);
+    A(&t->items, (T + 1) * N * 4 + 64);
     A(&t->action, T * N * 4);
     A(&t->forced, T * N * 4);
     A(&t->pold, T * N * 4);
@@ -1510,6 +1516,7 @@ int xh_trainer_create(xh_ctx *ctx, const xh_config *cfg, xh_trainer **out) {
     A(&t->pslab, (size_t)t->pslab_n * t->pslab_stride * 4);
     A(&t->vslab, (size_t)t->vslab_n * t->vslab_stride * 4);
     A(&t->vw0red, (size_t)c.value_h1 * (c.bins * c.dims + c.dims) * 4);
+    A(&t->vw0frag, xh::vnet_frag_bytes(t->env));
     A(&t->pgrads, (size_t)c.epochs * t->np * 4);
     A(&t->vgrad, (size_t)t->nv * 4);
     A(&t->logits, N * c.bins * 4);
@@ -1918,10 +1925,9 @@ int xh_trainer_kernel_info(xh_trainer *t, char *buf, size_t cap) {
     const std::string js = "{\"rollout_step\": " + kernel_json(t->last_rollout) +
                            ", \"policy_train\": " + kernel_json(t->last_train) +
                            ", \"value\": \"" +
-                           (t->cfg.algo != XH_PG &&
-                                    xh::value_fused(value_mlp(t, 0, nullptr))
-                                ? std::string("mlp3_fused")
-                                : std::string("gemm")) +
+                           std::string(t->cfg.algo != XH_PG
+                                           ? xh::value_kernel_name(value_mlp(t, 0, nullptr))
+                                           : "gemm") +
                            "\", \"train_grid\": " + std::to_string(t->pslab_n) +
                            ", \"train_grid_cap\": " +
                            std::to_string(t->cfg.train_grid_cap) +

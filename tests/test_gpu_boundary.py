@@ -241,7 +241,7 @@ def test_kernel_info_names_what_ran(ctx, monkeypatch, B, D, widths, train, roll,
         assert kt["kernel"].startswith("policy_train")
     assert k["overrides"] == {"XH_TRAIN_KERNEL": None, "XH_ROLLOUT_KERNEL": None,
                             "XH_VALUE_KERNEL": None}
-    assert k["value"] == "mlp3_fused"
+    assert k["value"] == "vnet_bf16"
     tr.close()
     if train:
         monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")

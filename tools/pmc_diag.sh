@@ -1,9 +1,11 @@
 #!/bin/bash
-# Diagnostic SQ counter passes of the config-3 bench's train kernel for a
+# Diagnostic SQ counter passes of a bench configuration's kernels for a
 # list of libraries (product and XH_LIB_PATH variants): wave-cycle
 # breakdown (waits, active VALU / LDS / misc), instruction fetch and LDS
-# queue levels.  Prints per-kernel means of the train kernel per pass.
+# queue levels.  Prints per-kernel means per pass for the kernels whose name
+# contains one of the KSUB substrings (default: the train kernel).
 #   LIBS="dependence_free_rl_amd/libxylo_hip.so build/abl2/libxylo_hip.so" bash tools/pmc_diag.sh
+#   CONFIG=5 KSUB="vnet_forward vnet_backward" bash tools/pmc_diag.sh
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,20 +20,24 @@ for lib in ${LIBS:-dependence_free_rl_amd/libxylo_hip.so}; do
     D=gpurun_out/pmcdiag_${n}_$p
     rm -rf $D
     XH_LIB_PATH=$lib timeout -s KILL 120 rocprofv3 --pmc $pc --output-format csv -d $D -o run \
-      -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $D.log 2>&1 || { tail -5 $D.log; exit 1; }
+      -- python3 bench.py --config ${CONFIG:-3} --steps 2 --warmup 1 --no-cpu-baseline > $D.log 2>&1 || { tail -5 $D.log; exit 1; }
   done
-  python3 - "$lib" $n <<'PY'
-import csv, glob, sys, collections
+  KSUB="${KSUB:-policy_train}" python3 - "$lib" $n <<'PY'
+import csv, glob, os, sys, collections
 lib, n = sys.argv[1], sys.argv[2]
-agg = collections.defaultdict(list)
+subs = os.environ["KSUB"].split()
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in (1, 2, 3):
     for f in glob.glob("gpurun_out/pmcdiag_%s_%d/**/*counter_collection.csv" % (n, p), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "policy_train" in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            for sub in subs:
+                if sub in r["Kernel_Name"]:
+                    agg[sub][r["Counter_Name"]].append(float(r["Counter_Value"]))
 print(lib)
-for k in sorted(agg):
-    v = agg[k]
-    print("  %-28s %16.0f" % (k, sum(v) / len(v)))
+for sub in subs:
+    print(" ", sub)
+    for k in sorted(agg[sub]):
+        v = agg[sub][k]
+        print("    %-28s %16.0f" % (k, sum(v) / len(v)))
 PY
 done
