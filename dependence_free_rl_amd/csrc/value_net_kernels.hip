@@ -60,12 +60,28 @@ __device__ __forceinline__ float sbyte(unsigned w, int b) {
 }
 
 // ---------------------------------------------------------------- W0 prep --
-// W0 / kCapacity on the reduced observation (reduce_w0_kernel's column sums,
-// ascending bins), three exact bf16 parts, in the forward's B-fragment
-// order: frag[(p * 2 + cb) * nkb + kb][lane] = part p of
-// [n = 32 cb + (lane & 31)][k = 16 kb + 8 (lane >> 5) + j], j = 0..7.
-__global__ void w0_frag_kernel(const float *W0, int in, int B, int D, int nkb,
-                               bf16x8 *frag) {
+// The item columns of W0 on the reduced observation: isum[n][c] = sum over
+// bins of W0[n][b 2D + D + c] (reduce_w0_kernel's sum, here in a fixed tree
+// order), one workgroup per (n, c): one round of loads instead of B
+// dependent ones per lane.
+__global__ __launch_bounds__(256) void w0_item_kernel(const float *W0, int in, int B,
+                                                      int D, float *isum) {
+  __shared__ float ws[4];
+  const int n = blockIdx.x / D, c = blockIdx.x - n * D;
+  const float *col = W0 + (size_t)n * in + D + c;
+  float v = 0.0f;
+  for (int b = threadIdx.x; b < B; b += 256) v += col[b * 2 * D];
+  v = seg_sum<64>(v);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) isum[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+}
+// W0 / kCapacity on the reduced observation, three exact bf16 parts, in the
+// forward's B-fragment order: frag[(p * 2 + cb) * nkb + kb][lane] = part p
+// of [n = 32 cb + (lane & 31)][k = 16 kb + 8 (lane >> 5) + j], j = 0..7
+// (k >= K: zero).
+__global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B, int D,
+                               int nkb, bf16x8 *frag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * nkb * 64) return;
   const int lane = i & 63, kb = (i >> 6) % nkb, cb = (i >> 6) / nkb;
@@ -77,20 +93,10 @@ __global__ void w0_frag_kernel(const float *W0, int in, int B, int D, int nkb,
   for (int j = 0; j < 8; ++j) {
     const int k = k0 + j;
     float w = 0.0f;
-    if (k < BD) {
+    if (k < BD)
       w = Wn[(k / D) * 2 * D + k % D];
-    } else if (k < K) {  // ascending bins; 16 loads in flight per batch
-      const float *c = Wn + D + (k - BD);
-      int b = 0;
-      for (; b + 16 <= B; b += 16) {
-        float t[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) t[u] = c[(b + u) * 2 * D];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) w += t[u];
-      }
-      for (; b < B; ++b) w += c[b * 2 * D];
-    }
+    else if (k < K)
+      w = isum[n * D + (k - BD)];
     split3(w * (1.0f / (float)kCapacity), hi[j], mid[j], lo[j]);
   }
   const size_t f = ((size_t)cb * nkb + kb) * 64 + lane, ps = (size_t)2 * nkb * 64;
@@ -610,7 +616,9 @@ static int vnet_nkc(const EnvDesc &e) {
   return 0;
 }
 
-size_t vnet_frag_bytes(const EnvDesc &e) { return (size_t)3 * 2 * vnet_nkb(e) * 64 * 16; }
+// W0's fragments, then the item-column sums [64][D]
+static size_t vnet_frag_only(const EnvDesc &e) { return (size_t)3 * 2 * vnet_nkb(e) * 64 * 16; }
+size_t vnet_frag_bytes(const EnvDesc &e) { return vnet_frag_only(e) + 64 * 3 * 4; }
 
 bool vnet_shape_ok(const MlpArgs &a) {
   const int BD = a.env.B * a.env.D;
@@ -630,8 +638,11 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   const int nkb = vnet_nkb(a.env);
   const int in = a.w[0];
   bf16x8 *frag = (bf16x8 *)a.w0frag;
+  float *isum = (float *)((char *)a.w0frag + vnet_frag_only(a.env));
+  hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
+                     a.env.B, a.env.D, isum);
   hipLaunchKernelGGL(w0_frag_kernel, dim3((2 * nkb * 64 + 255) / 256), dim3(256), 0, s,
-                     a.params, in, a.env.B, a.env.D, nkb, frag);
+                     a.params, (const float *)isum, in, a.env.B, a.env.D, nkb, frag);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int o1 = layer_off(a.w, 1), o2 = layer_off(a.w, 2);
