@@ -801,12 +801,21 @@ __device__ __forceinline__ void wave_logits_split(const char *lds,
         t1 = mfma32(wa, xb[s1], t1);
       }
       f16x8 bfr[2][2];
+      {
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        u32x4_t hb[2], lb[2];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        _Float16 p0, p1;
-        split2h(relu(t1[j]), p0, p1);
-        bfr[j >> 3][0][j & 7] = p0;
-        bfr[j >> 3][1][j & 7] = p1;
+        for (int jj = 0; jj < 8; ++jj) {
+          unsigned h2, l2;
+          split2h_x2(relu(t1[2 * jj]), relu(t1[2 * jj + 1]), h2, l2);
+          hb[jj >> 2][jj & 3] = h2;
+          lb[jj >> 2][jj & 3] = l2;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bfr[s][0] = __builtin_bit_cast(f16x8, hb[s]);
+          bfr[s][1] = __builtin_bit_cast(f16x8, lb[s]);
+        }
       }
 #pragma unroll
       for (int ot = 0; ot < S::NOT; ++ot) {

@@ -223,6 +223,21 @@ __device__ __forceinline__ void split2h(float x, _Float16 &hi, _Float16 &lo) {
   hi = (_Float16)x;
   lo = (_Float16)(x - (float)hi);
 }
+// split2h of two values, packed: hi2 = {hi(x0), hi(x1)} (v_cvt_pk_f16_f32,
+// round to nearest), lo2 = {lo(x0), lo(x1)} by v_fma_mixlo / mixhi_f16:
+// x * 1 - hi with hi read as f16 (op_sel_hi) is exact in f32 and rounded once
+// to f16, the same lo as split2h, in one instruction per value instead of a
+// convert back, a subtract and a convert (the compiler does not form the mix
+// from the subtract)
+__device__ __forceinline__ void split2h_x2(float x0, float x1, unsigned &hi2,
+                                           unsigned &lo2) {
+  typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+  hi2 = __builtin_bit_cast(unsigned, f16x2_t{(_Float16)x0, (_Float16)x1});
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lo2) : "v"(x0), "v"(hi2));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(lo2)
+      : "v"(x1), "v"(hi2));
+}
 // 2^(14 - e) for a maximum m <= 2^e (frexp); e clamped so that products of
 // two scales and their inverses stay normal f32
 __device__ __forceinline__ float f16_scale_for(float m) {
