@@ -777,7 +777,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // B: layer 1 of group gi -> the H1 image (f16 pairs), block b = (t, q)
     // of four rows at a time; the values are recomputed where DH needs them
     auto layer1 = [&](int gi) {
-      typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
       f32x16s pre[2];
       l1_mfma(gi, pre);
 #pragma unroll
@@ -786,12 +785,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
         unsigned hi[2], lo[2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-          // f16 pairs: v_cvt_pk_f16_f32, the remainders exact in f32
-          const float h0 = relu(pre[t][4 * q + 2 * p]), h1 = relu(pre[t][4 * q + 2 * p + 1]);
-          const f16x2 y = {(_Float16)h0, (_Float16)h1};
-          const f16x2 z = {(_Float16)(h0 - (float)y[0]), (_Float16)(h1 - (float)y[1])};
-          hi[p] = __builtin_bit_cast(unsigned, y);
-          lo[p] = __builtin_bit_cast(unsigned, z);
+          // f16 pairs: v_cvt_pk_f16_f32, the remainders by v_fma_mix (exact)
+          split2h_x2(relu(pre[t][4 * q + 2 * p]), relu(pre[t][4 * q + 2 * p + 1]), hi[p], lo[p]);
         }
         st4h(vwH[q] + 8192 * t, __builtin_bit_cast(f16x4, u32x2{hi[0], hi[1]}));
         st4h(vwH[q] + kImg + 8192 * t, __builtin_bit_cast(f16x4, u32x2{lo[0], lo[1]}));

@@ -556,16 +556,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
   };
   // H1 values (C layout, r-tile rt) scaled by S_H -> the two f16 part images
   auto store_h1 = [&](const f32x4 &t, int sb, int rt) {
-    f16x4 ph, pl;
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    u32x2_t ph, pl;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      _Float16 x0, x1;
-      split2h(t[u] * SH, x0, x1);
-      ph[u] = x0;
-      pl[u] = x1;
+    for (int u = 0; u < 2; ++u) {
+      unsigned h2, l2;
+      split2h_x2s(t[2 * u], t[2 * u + 1], SH, h2, l2);
+      ph[u] = h2;
+      pl[u] = l2;
     }
-    st4h(sb + L_H1 + 4096 * rt, ph);
-    st4h(sb + L_H1 + kImg + 4096 * rt, pl);
+    st4h(sb + L_H1 + 4096 * rt, __builtin_bit_cast(f16x4, ph));
+    st4h(sb + L_H1 + kImg + 4096 * rt, __builtin_bit_cast(f16x4, pl));
   };
   // layer 1 (C layout) of the group in slot s, all four r-tiles -> H1 image
   auto layer1_all = [&](int s, int stb) {

@@ -223,6 +223,19 @@ __device__ __forceinline__ void split2h(float x, _Float16 &hi, _Float16 &lo) {
   hi = (_Float16)x;
   lo = (_Float16)(x - (float)hi);
 }
+// split2h of (a0 s, a1 s), packed, for a power-of-two s (a s exact in f32):
+// hi by v_fma_mixlo / mixhi_f16 (a s + 0 rounded once to f16: the same as
+// converting the f32 product), lo as split2h_x2; four instructions per pair,
+// writing both halves of each word (no packing afterwards)
+__device__ __forceinline__ void split2h_x2s(float a0, float a1, float s, unsigned &hi2,
+                                            unsigned &lo2) {
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(hi2) : "v"(a0), "v"(s));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(hi2) : "v"(a1), "v"(s));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(lo2) : "v"(a0), "v"(s), "v"(hi2));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(lo2)
+      : "v"(a1), "v"(s), "v"(hi2));
+}
 // split2h of two values, packed: hi2 = {hi(x0), hi(x1)} (v_cvt_pk_f16_f32,
 // round to nearest), lo2 = {lo(x0), lo(x1)} by v_fma_mixlo / mixhi_f16:
 // x * 1 - hi with hi read as f16 (op_sel_hi) is exact in f32 and rounded once
