@@ -531,8 +531,11 @@ int xh_trainer_reset_timing(xh_trainer *t);
  *        "bf16_products_per_f32_product": p for "bf16_split", else null,
  *        "peak_tflops": the dense MFMA peak of that arithmetic on MI355X
  *        (2500 / p, or 157.3)}
- *   V = "mlp3_fused" (the Fin -> 64 -> 32 -> 1 value net in three launches
- *   per update) or "gemm" (layer by layer, other widths),
+ *   V = "vnet_bf16" (the Fin -> 64 -> 32 -> 1 value net on exact bf16
+ *   splits: two forwards and one fused backward per update, B*D % 16 == 0,
+ *   B*D + D < 416), "mlp3_fused" (the same net on the f32 fused kernels:
+ *   XH_VALUE_KERNEL=mlp3, or shapes the bf16 kernels do not take) or "gemm"
+ *   (layer by layer: other widths, XH_VALUE_KERNEL=gemm),
  *   G = the train grid (workgroups, = gradient slabs), C = xh_config
  *   train_grid_cap.
  * "overrides" lists the diagnostic environment variables that steer kernel
