@@ -884,7 +884,12 @@ __global__ __launch_bounds__(64 * roll_split_waves<S>(), roll_split_occ<S>()) vo
   // bin = lane when G = 1
   const int eoff = S::G == 2 ? h : 0, seg0 = S::G == 2 ? 32 * h : 0;
   const int bin = S::G == 2 ? lr : lane;
-  for (int g = blockIdx.x * wpb + w; g < ngroups; g += gridDim.x * wpb) {
+  // this workgroup's groups: a contiguous block of ceil(ngroups / grid),
+  // dealt round-robin to its waves, so that every CU steps the same number
+  // (the grid-strided order gave a sixth of the CUs one round more)
+  const int per = (ngroups + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int g_end = min(ngroups, ((int)blockIdx.x + 1) * per);
+  for (int g = (int)blockIdx.x * per + w; g < g_end; g += wpb) {
     const int e0 = g * S::G, env = e0 + eoff;
     RowRaw<S> cur;
     fetch_rows<S>(a.b, a.src_slot > 0 ? a.src_slot : a.t, e0, cur);
@@ -1244,7 +1249,13 @@ __global__ __launch_bounds__(64 * kRollWavesS128, 3) void rollout_split128_kerne
   const int wpb = blockDim.x >> 6;
   const int N = a.b.N;
   const int t_last = a.t + (a.nsteps > 1 ? a.nsteps : 1) - 1;
-  for (int env = blockIdx.x * wpb + w; env < N; env += gridDim.x * wpb) {
+  // this workgroup's envs: a contiguous block of ceil(N / grid), dealt
+  // round-robin to its waves, so that every CU steps the same number (the
+  // grid-strided order gave a third of the CUs six rounds against 5.33 on
+  // average at config 5)
+  const int per = (N + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int env_end = min(N, ((int)blockIdx.x + 1) * per);
+  for (int env = (int)blockIdx.x * per + w; env < env_end; env += wpb) {
     // slot t's rows of this lane: bins hg * 64 + rt * 32 + lr (the sampler's
     // lane 32 rt + lr, slot hg), from global for slot a.t, then from the
     // sampler's registers (this half's value and the partner half's)
