@@ -27,7 +27,8 @@
 //                   -> partial logits over its o
 //   matrix  SM(g)   softmax + loss gradient g of the 64 rows (every matrix
 //                   wave, from the four partial logits), dW3 / db2 sums,
-//                   relu masks -> mask images ([r][o], bf16 and f16)
+//                   relu masks -> the mask image ([r][o], 0 / 2.0: bf16 and
+//                   f16 alike)
 //   vector  DH(g)   dH1 = M (S_D W2') (32 MFMAs: its 32 features i), dW1 /
 //                   db1 / item sums; g (x) H1 -> the split image ([i][r])
 //   matrix  DW(g)   dW2 += M^T (g (x) H1) (48 MFMAs: its 32 features i)
@@ -41,8 +42,10 @@
 // W2' pair 64, dH1 accumulators 32, two groups' H1 64).
 //
 // LDS (dynamic, base 0): g (x) H1 three bf16 parts [128 i][64 r] (48 KB), H1
-// two f16 parts [64 r][128 i] (32 KB), relu masks bf16 + f16 [64 r][128 o]
-// in two slots (64 KB), then f32 vectors; image layout spec8_layout.h.
+// two f16 parts [64 r][128 i] (32 KB), relu masks [64 r][128 o] (0x4000 = 2.0
+// as bf16 and as f16)
+// in two slots (32 KB apart, 16 KB used), then f32 vectors; image layout
+// spec8_layout.h.
 #include <cstdlib>
 #include <type_traits>
 
@@ -101,7 +104,7 @@ constexpr int kThreads = 512;
 constexpr int kImg = 16384;        // one [128][64] / [64][128] 16-bit image
 constexpr int L_GH = 0;            // g (x) H1: hi, mid, lo
 constexpr int L_H1 = 3 * kImg;     // H1: hi, lo
-constexpr int L_MK = 5 * kImg;     // masks: slot s bf16 at + 2 kImg s, f16 + kImg
+constexpr int L_MK = 5 * kImg;     // masks: slot s at + 2 kImg s (the second kImg unused)
 constexpr int L_F = 9 * kImg;
 constexpr int F_B2 = 0;            // [128] b2 S2 (layer 2's accumulator input)
 constexpr int F_W3 = F_B2 + kH;    // [128] w3 / S2 (unscales the partial logits)
@@ -529,17 +532,18 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       acc3[e] = fmaf(gm, v, acc3[e]);
       accb2[e] += gm;
     };
-    // relu masks of block (t, q), bf16 (1.0 = 0x3F80) and f16 (0x3C00) -> slot ms
+    // relu masks of block (t, q) as 0 / 0x4000 -> slot ms: 0x4000 is 2.0 both
+    // as bf16 (dW2's A operand) and as f16 (dH1's), so one image serves both
+    // MFMA types (the factor 2 is taken back exactly at the write-outs)
     auto mask_q = [&](const f32x16s (&c)[2], int ms, int t, int q) {
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
       const int mb = 2 * kImg * ms;  // (mwb holds L_MK)
       unsigned m[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) m[u] = c[t][4 * q + u] > 0.0f ? 1u : 0u;
-      const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
-                        (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
+      const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x4000u),
+                        (unsigned)__umul24(m[2] | (m[3] << 16), 0x4000u)};
       st4(mb + 8192 * t + mwb[q], __builtin_bit_cast(bf16x4, mm));
-      st4h(mb + kImg + 8192 * t + mwb[q], __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
     };
     // dW2 += M^T (S_H g (x) H1) of the group whose masks are in slot ms:
     // 16 steps (K-step ks = st / 4 of 16 rows, o-tile mt = st % 4) of three
@@ -644,7 +648,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     }
 
     // ---- write-out (every entry has exactly one producing lane)
-    const float rSH = 1.0f / SH;
+    const float rSH = 0.5f / SH;  // (the masks were 2.0)
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -737,7 +741,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     }
     // image stores (lane row i, values r = 32 t + 8 q + 4 h ..; + 1024 t):
     // the g (x) H1 image (region base 0) and the H1 image; dH1's A operand
-    // (f16 mask images, lane row r = 32 t + l31)
+    // (the mask image read as f16, lane row r = 32 t + l31)
     int vwb[4], vwH[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -746,8 +750,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       // i = 32 v + 8 q + 4 h ..
       vwH[q] = opaque(wr_base(l31, q, h, 4) + 1024 * v + L_H1);
     }
-    const int rbm0 = opaque(rd_base(l31, 0, h, 4) + L_MK + kImg),
-              rbm1 = opaque(rd_base(l31, 1, h, 4) + L_MK + kImg);
+    const int rbm0 = opaque(rd_base(l31, 0, h, 4) + L_MK),
+              rbm1 = opaque(rd_base(l31, 1, h, 4) + L_MK);
     float w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
 
     // S_H pre-activations of layer 1 of group gi (its bins in slot gi & 3)
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // 4b + 3, its bins and g two blocks ahead (a ring of three indexed by the
     // unrolled block).  dh stays in registers for B's dW1.  gpar = gi & 1.
     auto dh_gh = [&](int gi, int gpar, f32x16s (&hk)[2], f32x16s (&dh)[2]) {
-      const int mb = 2 * kImg * gpar;  // f16 masks of slot gpar (rbm holds L_MK + kImg)
+      const int mb = 2 * kImg * gpar;  // the masks of slot gpar, read as f16 (rbm holds L_MK)
       const float *gv = lf + F_G + 192 * gpar;
       const float *xv = lf + F_X + (gi & 3) * 128;
       const float b1 = b1_of(gi);
@@ -954,10 +958,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     float tw1 = w1 + __shfl_xor(w1, 32, kWave);
     float va = sa + __shfl_xor(sa, 32, kWave);
     float vb = sb + __shfl_xor(sb, 32, kWave);
-    tw0 *= 1.0f / SD;
-    tw1 *= 1.0f / SD;
-    va *= 1.0f / SD;
-    vb *= 1.0f / SD;
+    // (dH1 was in units of S_D, times the masks' 2)
+    tw0 *= 0.5f / SD;
+    tw1 *= 0.5f / SD;
+    va *= 0.5f / SD;
+    vb *= 0.5f / SD;
     if (h == 0) {
       slab[PL.oW1() + fi * kF0 + 0] = tw0;
       slab[PL.oW1() + fi * kF0 + 1] = tw1;
