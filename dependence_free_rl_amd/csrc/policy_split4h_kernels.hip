@@ -72,8 +72,8 @@ constexpr int kNW = 4;                   // waves
 constexpr int kThreads = 64 * kNW;
 constexpr int kImg = 64 * kImgRow;       // one 64-row part image, 16 KB
 constexpr int L_H1 = 0;                  // H1 as two f16 parts (S_H)
-constexpr int L_MASK = 2 * kImg;         // bf16 mask (dW2's A operand)
-constexpr int L_MASKH = 3 * kImg;        // f16 mask (dH1's A operand)
+constexpr int L_MASK = 2 * kImg;         // relu mask (0 / 2.0: dW2 bf16, dH1 f16)
+// (3 * kImg: the f16 mask image before the one-image masks, unused)
 constexpr int L_F = 4 * kImg;
 constexpr int F_W1T = 0;                 // [64 i]: W1[i][0], the bin column
 constexpr int F_B1F = F_W1T + kH;        // [2 items][64]: b1 + the item's part
@@ -689,19 +689,20 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) hT[h][jj] = relu(fmaf(gx0[h][jj], w1a, b1tA));
       } else if (k >= 8 && k < 12) {
-        // r-tile rt: the relu masks -> the bf16 and f16 mask images, dW3 / db2
-        // (pre-activations in units of S2) from the same mask bits
+        // r-tile rt: the relu masks -> the mask image (0 / 0x4000: 2.0 as bf16
+        // for dW2 and as f16 for dH1; the factor 2 is taken back exactly at
+        // the write-out), dW3 / db2 (pre-activations in units of S2) from the
+        // same mask bits
         const int rt = k - 8;
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         unsigned m[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
-        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
-        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
-        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
-                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
+        // times the 2.0 bits by the full-rate 24-bit multiply (the 32-bit one
+        // is quarter rate)
+        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x4000u),
+                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x4000u)};
         st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const float v = pre_cur[rt][jj];
@@ -758,7 +759,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
                    (trm1 ^ (32 * ot)) + L_MASK + 8192 * ks);
         } else {
           const int rt = d >> 1, s = d & 1;
-          A = ld8((rdb ^ (64 * s)) + L_MASKH + 4096 * rt);  // f16 bits
+          A = ld8((rdb ^ (64 * s)) + L_MASK + 4096 * rt);  // read as f16
         }
       };
       // dW1 / db1 / item sums of value jj of r-tile rt (T layout; r-tiles 0,
@@ -908,7 +909,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int o = 16 * ot + 4 * G + j;
-      slab[PL.oW2() + o * kH + 16 * w + li] = accW2[ot][j] * w3g[o];
+      slab[PL.oW2() + o * kH + 16 * w + li] = (accW2[ot][j] * 0.5f) * w3g[o];
     }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -932,9 +933,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split4h_kernel(
     va += __shfl_xor(va, 32, kWave);
     vb += __shfl_xor(vb, 32, kWave);
     // dH1 was in units of S_D
-    tw0 *= 1.0f / SD;
-    va *= 1.0f / SD;
-    vb *= 1.0f / SD;
+    tw0 *= 0.5f / SD;  // (and the masks were 2.0)
+    va *= 0.5f / SD;
+    vb *= 0.5f / SD;
     if (G == 0) {
       const int i = 16 * w + li;
       slab[PL.oW1() + i * kF0 + 0] = tw0;

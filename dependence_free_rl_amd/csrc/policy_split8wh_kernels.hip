@@ -141,7 +141,7 @@ constexpr int kImg = 64 * kImgRow;  // one 64-row part image, 16 KB
 // operand, row reads), then f32.  W2 / W2' live in registers as f16 pairs.
 constexpr int L_H1 = 0;
 constexpr int L_MASK = 2 * kImg;
-constexpr int L_MASKH = 3 * kImg;
+// (3 * kImg: the f16 mask image before the one-image masks, unused)
 constexpr int L_F = 4 * kImg;
 constexpr int F_W1T = 0;               // [2 k][128 i]: W1[i][k], the bin columns
 constexpr int F_B1F = F_W1T + 2 * kH;  // [2 items][128]: b1 + the item's part
@@ -790,9 +790,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
           bq0[2][4 * h + jj] = p2;
         }
       } else if (k >= 20 && k < 24) {
-        // the relu masks of r-tile k - 20 (C layout) -> the bf16 and f16
-        // mask images (1.0 = 0x3F80 / 0x3C00: the f16 bits are the bf16
-        // bits & 0x3C00)
+        // the relu masks of r-tile k - 20 (C layout) -> the mask image (0 /
+        // 0x4000: 2.0 as bf16 for dW2 and as f16 for dH1; the factor 2 is
+        // taken back exactly at the write-outs)
         const int rt = k - 20;
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #if XH_8WH_IMASK
@@ -801,20 +801,17 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
           m[jj] = (unsigned)relu_bit(pre_cur[rt][jj]);
-        // times the bf16 1.0 bits by the full-rate 24-bit multiply (the
-        // 32-bit one is quarter rate), the f16 1.0 bits masked out of them
-        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x3F80u),
-                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x3F80u)};
+        // times the 2.0 bits by the full-rate 24-bit multiply (the 32-bit
+        // one is quarter rate)
+        const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x4000u),
+                          (unsigned)__umul24(m[2] | (m[3] << 16), 0x4000u)};
         st4(stb + L_MASK + 4096 * rt, __builtin_bit_cast(bf16x4, mm));
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mm & 0x3C003C00u));
 #else
         bf16x4 mk;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
-          mk[jj] = pre_cur[rt][jj] > 0.0f ? (__bf16)1.0f : (__bf16)0.0f;
+          mk[jj] = pre_cur[rt][jj] > 0.0f ? (__bf16)2.0f : (__bf16)0.0f;
         st4(stb + L_MASK + 4096 * rt, mk);
-        const u32x2 mb = __builtin_bit_cast(u32x2, mk) & 0x3C003C00u;
-        st4h(stb + L_MASKH + 4096 * rt, __builtin_bit_cast(f16x4, mb));
 #endif
       } else if (k == 36) {
         w3 = lds4v(lf + F_W3 + fo);  // for the partial logits after layer 2
@@ -859,7 +856,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
                    (trm1 ^ (32 * ot)) + L_MASK + 8192 * ks);
         } else {
           const int rt = b >> 2, s = b & 3;
-          A = ld8((rdb ^ (64 * s)) + L_MASKH + 4096 * rt);  // f16 bits
+          A = ld8((rdb ^ (64 * s)) + L_MASK + 4096 * rt);  // read as f16
         }
       };
       // dW1 / db1 / item sums of value jj of r-tile rt (T layout)
@@ -1009,7 +1006,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int o = 16 * ot + 4 * G + j;
-      slab[PL.oW2() + o * kH + 16 * w + li] = accW2[ot][j] * w3g[o];
+      slab[PL.oW2() + o * kH + 16 * w + li] = (accW2[ot][j] * 0.5f) * w3g[o];
     }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1037,10 +1034,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_split8wh_kernel(
     va += __shfl_xor(va, 32, kWave);
     vb += __shfl_xor(vb, 32, kWave);
     // dH1 was in units of S_D
-    tw0 *= 1.0f / SD;
-    tw1 *= 1.0f / SD;
-    va *= 1.0f / SD;
-    vb *= 1.0f / SD;
+    tw0 *= 0.5f / SD;  // (and the masks were 2.0)
+    tw1 *= 0.5f / SD;
+    va *= 0.5f / SD;
+    vb *= 0.5f / SD;
     if (G == 0) {
       const int i = 16 * w + li;
       slab[PL.oW1() + i * kF0 + 0] = tw0;
