@@ -137,6 +137,9 @@ __device__ __forceinline__ f16x8 ld8h(int off) {
 __device__ __forceinline__ void st4(int off, bf16x4 v) {
   *(lbf16x4 *)(size_t)(unsigned)off = v;
 }
+__device__ __forceinline__ void st8h(int off, f16x8 v) {
+  *(lf16x8 *)(size_t)(unsigned)off = v;
+}
 __device__ __forceinline__ void st4h(int off, f16x4 v) {
   *(lf16x4 *)(size_t)(unsigned)off = v;
 }
@@ -283,13 +286,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     const int s = role_idx;  // outputs o in [32 s, 32 s + 32) for layer 2 /
                              // SM, features i in [32 s, 32 s + 32) for dW2
     // W2 (S_W) as f16 pairs, A operand of layer 2: lane row o = 32 s + l31,
-    // K-step ks: k = i = 16 ks + 8 h + e
+    // K-step ks: k = the H1 image's column 16 ks + 8 h + e, which holds
+    // feature i = 32 (ks >> 1) + 16 h + 8 (e >> 2) + 4 (ks & 1) + (e & 3)
+    // (the image's column order: each vector lane stores its 16 features of
+    // a row as two whole 16-byte chunks, see layer1)
     f16x8 wl[8][2];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      const float4 *src = reinterpret_cast<const float4 *>(
-          P + PL.oW2() + (32 * s + l31) * kH + 16 * ks + 8 * h);
-      const float4 v0 = src[0], v1 = src[1];
+      const float *row = P + PL.oW2() + (32 * s + l31) * kH + 32 * (ks >> 1) + 16 * h + 4 * (ks & 1);
+      const float4 v0 = *reinterpret_cast<const float4 *>(row),
+                   v1 = *reinterpret_cast<const float4 *>(row + 8);
       const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -304,8 +310,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // operand (g (x) H1 image, lane column i = 32 s + l31, row reads), the
     // mask stores from layer 2's C layout (lane row r = 32 t + l31, o = 32 s +
     // 8 q + 4 h ..; + 8192 t)
-    // (layer 2's B operand: row reads of the [r][i] H1 image, lane row r =
-    // 32 t + l31, K-step ks: i = 16 ks + 8 h ..; + 8192 t + 1024 (ks >> 1))
+    // (layer 2's B operand: row reads of the [r][column] H1 image, lane row
+    // r = 32 t + l31, K-step ks: columns 16 ks + 8 h ..; + 8192 t + 1024 (ks
+    // >> 1); the columns' features as in the W2 fragments above)
     const int rbH0 = opaque(rd_base(l31, 0, h, 4) + L_H1), rbH1 = opaque(rd_base(l31, 1, h, 4) + L_H1);
     const int trM0 = opaque(tr_base(l, 0) + L_MK), trM1 = opaque(tr_base(l, 1) + L_MK);
     const int rbg0 = rd_base(32 * s + l31, 0, h, 2) + L_GH,
@@ -742,14 +749,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // image stores (lane row i, values r = 32 t + 8 q + 4 h ..; + 1024 t):
     // the g (x) H1 image (region base 0) and the H1 image; dH1's A operand
     // (the mask image read as f16, lane row r = 32 t + l31)
-    int vwb[4], vwH[4];
+    int vwb[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      vwb[q] = opaque(wr_base(fi, q, h, 2) + L_GH);
-      // the H1 image is [r][i]: lane row r = 32 t + l31 (+ 8192 t), values
-      // i = 32 v + 8 q + 4 h ..
-      vwH[q] = opaque(wr_base(l31, q, h, 4) + 1024 * v + L_H1);
-    }
+    for (int q = 0; q < 4; ++q) vwb[q] = opaque(wr_base(fi, q, h, 2) + L_GH);
+    // the H1 image is [r][column]: lane row r = 32 t + l31 (+ 8192 t); this
+    // lane's features i = 32 v + 8 q + 4 h + u go to columns 32 v + 16 h + 8
+    // (q >> 1) + 4 (q & 1) + u, i.e. whole chunks 2 h and 2 h + 1 of column
+    // tile v (one ds_write_b128 each, conflict-free in the poff layout)
+    int vwH[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) vwH[j] = opaque(poff(l31, 32 * v + 16 * h + 8 * j, 4) + L_H1);
     const int rbm0 = opaque(rd_base(l31, 0, h, 4) + L_MK),
               rbm1 = opaque(rd_base(l31, 1, h, 4) + L_MK);
     float w0 = 0.0f, w1 = 0.0f, sa = 0.0f, sb = 0.0f;
@@ -784,16 +793,22 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       f32x16s pre[2];
       l1_mfma(gi, pre);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int t = b >> 2, q = b & 3;
-        unsigned hi[2], lo[2];
+      for (int b = 0; b < 4; ++b) {
+        // chunk j = b & 1 of r-tile t = b >> 1: blocks q = 2 j, 2 j + 1
+        const int t = b >> 1, j = b & 1;
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 hi, lo;
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int p = 0; p < 4; ++p) {
+          const int q = 2 * j + (p >> 1), u = 2 * (p & 1);
           // f16 pairs: v_cvt_pk_f16_f32, the remainders by v_fma_mix (exact)
-          split2h_x2(relu(pre[t][4 * q + 2 * p]), relu(pre[t][4 * q + 2 * p + 1]), hi[p], lo[p]);
+          unsigned h2, l2;
+          split2h_x2(relu(pre[t][4 * q + u]), relu(pre[t][4 * q + u + 1]), h2, l2);
+          hi[p] = h2;
+          lo[p] = l2;
         }
-        st4h(vwH[q] + 8192 * t, __builtin_bit_cast(f16x4, u32x2{hi[0], hi[1]}));
-        st4h(vwH[q] + kImg + 8192 * t, __builtin_bit_cast(f16x4, u32x2{lo[0], lo[1]}));
+        st8h(vwH[j] + 8192 * t, __builtin_bit_cast(f16x8, hi));
+        st8h(vwH[j] + kImg + 8192 * t, __builtin_bit_cast(f16x8, lo));
       }
     };
     // x0, x1 -> three bf16 parts each, as bf16 pairs: v_cvt_pk_bf16_f32 and

@@ -5,7 +5,7 @@
 # (e.g. "--algo klppo").
 set -o pipefail
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
 for v in product $NAMES; do
   if [ $v = product ]; then lib=dependence_free_rl_amd/libxylo_hip.so; else lib=build/$v/libxylo_hip.so; fi
   XH_LIB_PATH=$lib timeout -k 10 200 python bench.py --config ${CONFIG:-3} --steps 5 --warmup 2 --no-cpu-baseline $EXTRA \
