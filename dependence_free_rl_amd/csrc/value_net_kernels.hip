@@ -21,6 +21,8 @@
 // Observation layout: the reduced feature vector of dense_kernels.hip's
 // ObsRedRows (the B*D bin features, then the D item features once, their B
 // copies' weights summed), so layer 0's K = B*D + D.
+#include <cstdlib>
+
 #include "xh_device.h"
 #include "xh_kernels.h"
 
@@ -80,6 +82,29 @@ __global__ __launch_bounds__(256) void w0_item_kernel(const float *W0, int in, i
 // forward's B-fragment order: frag[(p * 2 + cb) * nkb + kb][lane] = part p
 // of [n = 32 cb + (lane & 31)][k = 16 kb + 8 (lane >> 5) + j], j = 0..7
 // (k >= K: zero).
+// isum[n][c] for B <= 64 inside one lane, in w0_item_kernel's order: its
+// seg_sum<64> is the balanced pairwise tree over the 64 lanes (zeros past B),
+// then + 0 for the empty waves, so the bits are the same
+__device__ __forceinline__ float item_sum_tree(const float *col, int D, int B) {
+  float r[4];
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int b = 16 * row + i;
+      v[i] = b < B ? col[b * 2 * D] : 0.0f;
+    }
+#pragma unroll
+    for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+      for (int i = 0; i < 16; i += 2 * w) v[i] = v[i] + v[i + w];
+    r[row] = v[0];
+  }
+  const float s = (r[0] + r[1]) + (r[2] + r[3]);
+  return (s + 0.0f) + (0.0f + 0.0f);
+}
+// isum == nullptr (B <= 64): the item sums computed here (one launch fewer)
 __global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B, int D,
                                int nkb, bf16x8 *frag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -96,7 +121,7 @@ __global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B
     if (k < BD)
       w = Wn[(k / D) * 2 * D + k % D];
     else if (k < K)
-      w = isum[n * D + (k - BD)];
+      w = isum ? isum[n * D + (k - BD)] : item_sum_tree(Wn + D + (k - BD), D, B);
     split3(w * (1.0f / (float)kCapacity), hi[j], mid[j], lo[j]);
   }
   const size_t f = ((size_t)cb * nkb + kb) * 64 + lane, ps = (size_t)2 * nkb * 64;
@@ -639,10 +664,20 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   const int in = a.w[0];
   bf16x8 *frag = (bf16x8 *)a.w0frag;
   float *isum = (float *)((char *)a.w0frag + vnet_frag_only(a.env));
-  hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
-                     a.env.B, a.env.D, isum);
+  // up to 64 bins the fragment kernel sums the item columns itself (config 2:
+  // one 4-us launch fewer per forward); at 128 the serial sums cost more
+  // (XH_W0_FUSE=0: always the separate item kernel; tests compare the two)
+  static const bool fuse_ok = [] {
+    const char *e = std::getenv("XH_W0_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  const bool fuse = fuse_ok && a.env.B <= 64;
+  if (!fuse)
+    hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
+                       a.env.B, a.env.D, isum);
   hipLaunchKernelGGL(w0_frag_kernel, dim3((2 * nkb * 64 + 255) / 256), dim3(256), 0, s,
-                     a.params, (const float *)isum, in, a.env.B, a.env.D, nkb, frag);
+                     a.params, fuse ? nullptr : (const float *)isum, in, a.env.B, a.env.D, nkb,
+                     frag);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int o1 = layer_off(a.w, 1), o2 = layer_off(a.w, 2);
@@ -669,7 +704,11 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   o.out = a.act[2];
   o.v_term = a.v_term && a.term_list ? a.v_term : nullptr;
   const int tiles = (a.max_rows + TM - 1) / TM;
-  const dim3 grid(tiles < 256 ? (tiles < 1 ? 1 : tiles) : 256);
+  // up to 512 workgroups (two per CU) where the kernel's registers allow two
+  // waves per SIMD (NKH <= 6: configs 2 / 3, value phase 0.055 -> 0.053 and
+  // 0.156 -> 0.133 ms per iteration); one tile each, so its prefetch idles
+  const int gcap = vnet_nkh(a.env) <= 6 ? 512 : 256;
+  const dim3 grid(tiles < gcap ? (tiles < 1 ? 1 : tiles) : gcap);
   switch (vnet_nkh(a.env)) {
 #define XH_VNET_FWD(n)                                                          \
   case n:                                                                       \

@@ -33,7 +33,11 @@ def test_value_kernels_against_gemm(ctx, monkeypatch, algo, B, D, widths, N, T):
     bufs = (BUF_V_STATE0, BUF_V_TERM, BUF_TARGETS, BUF_VALUE_GRAD, BUF_V_STATE,
             BUF_ADV)
 
-    def run(kernel):
+    def run(kernel, w0_fuse=None):
+        if w0_fuse is None:
+            monkeypatch.delenv("XH_W0_FUSE", raising=False)
+        else:
+            monkeypatch.setenv("XH_W0_FUSE", w0_fuse)
         if kernel:
             monkeypatch.setenv("XH_VALUE_KERNEL", kernel)
         else:
@@ -55,6 +59,13 @@ def test_value_kernels_against_gemm(ctx, monkeypatch, algo, B, D, widths, N, T):
     m3, km = run("mlp3")
     got, kg = run(None)
     assert (kr, km, kg) == ("gemm", "mlp3_fused", "vnet_bf16")
+    if B <= 64:
+        # the W0 fragments' item sums inside w0_frag_kernel (the default up
+        # to 64 bins) have the bits of the separate w0_item_kernel
+        sep, _ = run(None, w0_fuse="0")
+        for it, (x, y) in enumerate(zip(got, sep)):
+            for i, (a, b) in enumerate(zip(x, y)):
+                np.testing.assert_array_equal(a, b, err_msg="w0 fuse iteration %d item %d" % (it, i))
     worst = {}
     for it, (x, y, z) in enumerate(zip(got, ref, m3)):
         for i, (a, b, c) in enumerate(zip(x, y, z)):
