@@ -5,7 +5,10 @@
 //   * every lane base + loop immediate the kernel uses addresses the element
 //     the MFMA operand map / C layout asks for;
 //   * bank conflicts per access pattern by the lane groups and bank rules of
-//     MI355X_MICROARCH.md §LDS (stores 2-way, reads conflict-free).
+//     MI355X_MICROARCH.md §LDS (8-byte stores 2-way, 16-byte chunk stores and
+//     reads conflict-free);
+//   * the H1 image's column order (layer 1's chunk stores) is the inverse of
+//     layer 2's W2 fragment gather.
 // Prints one line per check and exits non-zero on the first failure.
 #include <cstdio>
 #include <cstdlib>
@@ -130,8 +133,44 @@ int main() {
           worst_tr = std::max(worst_tr, ways(contiguous(32), addr, 2, 64));
         }
   }
-  std::printf("stores: %d-way\nrow reads: %d-way\ntransposed reads: %d-way\n", worst_store,
-              worst_row, worst_tr);
+  // layer 1's H1 stores as whole 16-byte chunks (round 5): lane row x = X0
+  // + (l & 31), chunk j of column tile v: columns 32 v + 16 h + 8 j .. + 7
+  int worst_chunk = 0;
+  for (int X0 = 0; X0 < 64; X0 += 32)
+    for (int v = 0; v < 4; ++v)
+      for (int j = 0; j < 2; ++j) {
+        for (int l = 0; l < 64; ++l) {
+          const int x = X0 + (l & 31), h = l >> 5, y = 32 * v + 16 * h + 8 * j;
+          addr[l] = poff(l & 31, y, 4) + 8192 * (X0 / 32);
+          for (int e = 0; e < 8; ++e)
+            CHECK(addr[l] + 2 * e == poff(x, y + e, 4), "chunk store x%d y%d", x, y);
+          CHECK(addr[l] % 16 == 0, "chunk store alignment");
+        }
+        worst_chunk = std::max(worst_chunk, ways(b128_groups(), addr, 4, 64));
+      }
+  // the H1 image's column order: the vector lane's feature i = 32 v + 8 q + 4
+  // h + u goes to column 32 v + 16 h + 8 (q >> 1) + 4 (q & 1) + u; layer 2's
+  // W2 fragment column 16 ks + 8 h + e is gathered from feature 32 (ks >> 1)
+  // + 16 h + 8 (e >> 2) + 4 (ks & 1) + (e & 3): the two maps are inverse
+  {
+    std::vector<int> col_of(128), seen(128, 0);
+    for (int i = 0; i < 128; ++i) {
+      const int v = i >> 5, r = i & 31, q = r >> 3, h = (r >> 2) & 1, u = r & 3;
+      col_of[i] = 32 * v + 16 * h + 8 * (q >> 1) + 4 * (q & 1) + u;
+      seen[col_of[i]]++;
+    }
+    for (int c = 0; c < 128; ++c) {
+      CHECK(seen[c] == 1, "column order not a bijection at %d", c);
+      const int ks = c >> 4, hm = (c >> 3) & 1, e = c & 7;
+      const int f = 32 * (ks >> 1) + 16 * hm + 8 * (e >> 2) + 4 * (ks & 1) + (e & 3);
+      CHECK(col_of[f] == c, "W2 fragment column %d gathers feature %d (stored at %d)", c, f,
+            col_of[f]);
+    }
+    std::printf("column order: ok\n");
+  }
+  std::printf("stores: %d-way\nrow reads: %d-way\ntransposed reads: %d-way\nchunk stores: %d-way\n",
+              worst_store, worst_row, worst_tr, worst_chunk);
+  CHECK(worst_chunk == 1, "chunk stores %d-way", worst_chunk);
   CHECK(worst_store <= 2, "stores %d-way", worst_store);
   CHECK(worst_row == 1, "row reads %d-way", worst_row);
   CHECK(worst_tr == 1, "transposed reads %d-way", worst_tr);

@@ -23,3 +23,5 @@ def test_spec8_layout(tmp_path):
     assert "stores: 2-way" in out.stdout
     assert "row reads: 1-way" in out.stdout
     assert "transposed reads: 1-way" in out.stdout
+    assert "chunk stores: 1-way" in out.stdout
+    assert "column order: ok" in out.stdout
