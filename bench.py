@@ -64,7 +64,8 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 # split rollouts' layer 2 on f16 pairs: dense 2500 / 3.
 # Diagnostic variables that steer kernel selection (the bench refuses them
 # unless --allow-kernel-override is given):
-KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL", "XH_VALUE_KERNEL")
+KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL", "XH_VALUE_KERNEL",
+                    "XH_W0_FUSE")
 HBM_PEAK_GBS = 8000.0
 PHASE_ITERS = 3  # the phase-breakdown pass after the timed region
 
@@ -340,7 +341,8 @@ def main():
                          "config's; SURVEY 8(d)'s larger-T throughput point)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--allow-kernel-override", action="store_true",
-                    help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL / XH_VALUE_KERNEL are "
+                    help="run even if XH_TRAIN_KERNEL / XH_ROLLOUT_KERNEL / XH_VALUE_KERNEL / "
+                         "XH_W0_FUSE are "
                          "set (A/B measurements; the line records them)")
     ap.add_argument("--algo", choices=("ppo", "klppo", "ac"), default=None,
                     help="learner on the config's shape (default: the "

@@ -2,7 +2,8 @@
 # Paired A/B of one library under an environment switch: bench.py --config
 # $CONFIG with "$ENVA" and with "$ENVB" (e.g. ENVA="XH_W0_FUSE=0" ENVB=""),
 # alternating, REPS rounds; optional pytest files first (TESTS).  Each GPU
-# step has its own limit.
+# step has its own limit.  Kernel-selection switches need
+# EXTRA=--allow-kernel-override (bench.py refuses them otherwise).
 set -o pipefail
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
