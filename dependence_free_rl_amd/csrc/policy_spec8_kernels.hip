@@ -77,6 +77,14 @@
 // phase-B blocks (dW1, layer 1) across block boundaries
 // XH_SP8_GH2 (A/B builds): 1 splits a block's two pairs in one MFMA slot
 // (two independent chains interleaved) and stores in the next
+// XH_SP8_VFIRST (A/B builds): the vector role to the first (older) wave on
+// each SIMD, the matrix role to the second -- the older wave wins VALU issue
+// arbitration and the vector waves carry the VALU (policy_train phase 7.29 ->
+// 7.27 ms per iteration over three paired rounds; to adopt with the next
+// evidence refresh); 0 = the matrix role first, as the r05z evidence ran
+#ifndef XH_SP8_VFIRST
+#define XH_SP8_VFIRST 0
+#endif
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
 #endif
@@ -256,15 +264,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
   // (the loop's barriers order these LDS writes before their first reads)
 
   // ---- roles by SIMD: the first wave (lowest index) on each SIMD takes
-  // the matrix role, the second the vector role, so that every SIMD pairs
-  // one of each whatever order the hardware placed the waves in (HW_ID
-  // SIMD_ID, bits 5:4); any other placement falls back to waves 0-3 / 4-7.
+  // the matrix role, the second the vector role (XH_SP8_VFIRST=1 swaps
+  // them), so that every SIMD pairs one of each whatever order the hardware
+  // placed the waves in (HW_ID SIMD_ID, bits 5:4); any other placement falls
+  // back to waves 0-3 / 4-7.
   // s / v number the matrix / vector waves by their SIMD's rank.
   if (l == 0)
     reinterpret_cast<int *>(lf + F_SIMD)[w] =
         (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3);
   __syncthreads();
-  int is_matrix = w < 4, role_idx = w & 3;
+  int is_matrix = XH_SP8_VFIRST ? w >= 4 : w < 4, role_idx = w & 3;
   {
     const int *sid = reinterpret_cast<const int *>(lf + F_SIMD);
     int per[4] = {0, 0, 0, 0}, rank = 0;
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       per[su & 3]++;
     }
     if (per[0] == 2 && per[1] == 2 && per[2] == 2 && per[3] == 2) {
-      is_matrix = rank == 0;
+      is_matrix = XH_SP8_VFIRST ? rank == 1 : rank == 0;
       role_idx = sid[w];
     }
   }
