@@ -77,13 +77,12 @@
 // phase-B blocks (dW1, layer 1) across block boundaries
 // XH_SP8_GH2 (A/B builds): 1 splits a block's two pairs in one MFMA slot
 // (two independent chains interleaved) and stores in the next
-// XH_SP8_VFIRST (A/B builds): the vector role to the first (older) wave on
-// each SIMD, the matrix role to the second -- the older wave wins VALU issue
-// arbitration and the vector waves carry the VALU (policy_train phase 7.29 ->
-// 7.27 ms per iteration over three paired rounds; to adopt with the next
-// evidence refresh); 0 = the matrix role first, as the r05z evidence ran
+// XH_SP8_VFIRST: the vector role to the first (older) wave on each SIMD, the
+// matrix role to the second -- the older wave wins VALU issue arbitration and
+// the vector waves carry the VALU (policy_train phase 7.29 -> 7.27 ms per
+// iteration over three paired rounds); 0 = the matrix role first
 #ifndef XH_SP8_VFIRST
-#define XH_SP8_VFIRST 0
+#define XH_SP8_VFIRST 1
 #endif
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
@@ -264,10 +263,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
   // (the loop's barriers order these LDS writes before their first reads)
 
   // ---- roles by SIMD: the first wave (lowest index) on each SIMD takes
-  // the matrix role, the second the vector role (XH_SP8_VFIRST=1 swaps
+  // the vector role, the second the matrix role (XH_SP8_VFIRST; 0 swaps
   // them), so that every SIMD pairs one of each whatever order the hardware
   // placed the waves in (HW_ID SIMD_ID, bits 5:4); any other placement falls
-  // back to waves 0-3 / 4-7.
+  // back to waves 4-7 / 0-3.
   // s / v number the matrix / vector waves by their SIMD's rank.
   if (l == 0)
     reinterpret_cast<int *>(lf + F_SIMD)[w] =
