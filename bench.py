@@ -327,9 +327,144 @@ def _venv_done():
     return VENV_DONE
 
 
+_VISIBLE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                 "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+
+def visible_devices_no_hip():
+    """GPUs this process could open, counted WITHOUT initialising HIP (the
+    launcher parent must never touch the device: a process that has
+    initialised HIP may not start the ranks by exec, and the ranks must be
+    the first HIP users of their devices).  A GPU is a KFD topology node with
+    SIMDs whose DRM render node this process may open; a non-empty
+    *_VISIBLE_DEVICES list caps the count at its length."""
+    import glob
+    n = 0
+    for props in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        kv = {}
+        try:
+            with open(props) as f:
+                for line in f:
+                    p = line.split()
+                    if len(p) == 2:
+                        kv[p[0]] = p[1]
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue  # a CPU node
+        minor = kv.get("drm_render_minor")
+        if minor is not None and not os.access("/dev/dri/renderD%s" % minor,
+                                               os.R_OK | os.W_OK):
+            continue  # not passed into this container / cgroup
+        n += 1
+    for var in _VISIBLE_VARS:
+        v = os.environ.get(var, "").strip()
+        if v:
+            n = min(n, len([e for e in v.split(",") if e.strip()]))
+    return n
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start the N
+    rank processes here (one per GPU, the same contract torch.distributed.run
+    gives them: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, and
+    XH_RDZV_PORT for the torch-free rendezvous), relay rank 0's JSON line
+    (the children inherit stdout; only rank 0 prints) and exit with the worst
+    child status.  This process never initialises HIP and never execs."""
+    import signal
+    n = args.gpus
+    if not args.dry_run_ranks:
+        have = visible_devices_no_hip()
+        if have < n:
+            print("bench.py: --gpus %d needs %d devices, %d visible (KFD "
+                  "topology nodes with an accessible render node); not "
+                  "starting the ranks" % (n, n, have), file=sys.stderr)
+            return 3
+    port = _free_port()
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                XH_RDZV_PORT=str(port))
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)]
+                                      + argv, env=env))
+    rcs = [None] * n
+    failed = False
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0) and not failed:
+                    failed = True
+                    print("bench.py: rank %d exited with %d; stopping the "
+                          "others" % (i, rcs[i]), file=sys.stderr)
+                    for q in procs:
+                        if q.poll() is None:
+                            q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    worst = 0
+    for rc in rcs:
+        code = rc if rc >= 0 else 128 - rc
+        worst = max(worst, code)
+    return worst
+
+
+def dry_run_rank(rank, world, local):
+    """--dry-run-ranks: a rank's plumbing without the device -- its env, the
+    rendezvous (an id broadcast, barriers, the max-over-ranks of its wall
+    time) and rank 0's one line; stops before any HIP call."""
+    print("bench.py rank env: %s" % json.dumps(
+        {"RANK": rank, "LOCAL_RANK": local, "WORLD_SIZE": world,
+         "MASTER_ADDR": os.environ.get("MASTER_ADDR"),
+         "XH_RDZV_PORT": os.environ.get("XH_RDZV_PORT"), "pid": os.getpid()}),
+        file=sys.stderr, flush=True)
+    ranks = [{"rank": rank, "local_rank": local, "pid": os.getpid()}]
+    dt = 0.001 * (rank + 1)
+    if world > 1:
+        # the module file alone: the package's __init__ loads libxylo_hip.so
+        import importlib.util
+        spec = importlib.util.spec_from_file_location(
+            "xh_rendezvous", os.path.join(REPO, "dependence_free_rl_amd",
+                                          "rendezvous.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        rdzv = mod.Rendezvous(rank, world)
+        uid = rdzv.broadcast(bytes(range(128)) if rank == 0 else None)
+        assert uid == bytes(range(128))
+        rdzv.barrier()
+        got = rdzv.gather(json.dumps(ranks[0]).encode())
+        dt = rdzv.allreduce_max(dt)
+        rdzv.barrier()
+        rdzv.close()
+        if rank == 0:
+            ranks = [json.loads(g) for g in got]
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (rank plumbing only, no device)",
+                          "value": None, "n_gpus": world, "dry_run": True,
+                          "max_rank_time_s": dt, "ranks": ranks}), flush=True)
+    assert "dependence_free_rl_amd._lib" not in sys.modules  # no HIP loaded
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks = GPUs of this node (default: WORLD_SIZE, else "
+                         "1).  Without WORLD_SIZE in the environment, N > 1 "
+                         "starts the N rank processes itself")
+    ap.add_argument("--dry-run-ranks", action="store_true",
+                    help="start / join the ranks and their rendezvous, print "
+                         "rank 0's line, and stop before any HIP call")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
@@ -354,7 +489,8 @@ def main():
     ap.add_argument("--reference-lr", action="store_true",
                     help="raw lr on row sums as the reference (diverges at "
                          "this batch size; default: lr_scale_rows)")
-    args = ap.parse_args()
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
     set_over = {k: os.environ[k] for k in KERNEL_OVERRIDES if k in os.environ}
     if set_over and not args.allow_kernel_override:
         print("bench.py: kernel-selection override(s) set %s; unset them or "
@@ -373,9 +509,20 @@ def main():
         global T
         T = args.rollout_steps
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and args.gpus != int(env_world):
+            print("bench.py: --gpus %d disagrees with WORLD_SIZE=%s" % (
+                args.gpus, env_world), file=sys.stderr)
+            sys.exit(2)
+    elif (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args, argv))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run_ranks:
+        sys.exit(dry_run_rank(rank, world, local))
     rdzv = None
     uid = None
     device = local
@@ -389,8 +536,17 @@ def main():
         from dependence_free_rl_amd import Context, device_count
         from dependence_free_rl_amd.rendezvous import Rendezvous
         ndev = device_count()
-        if ndev > 0 and local >= ndev:  # launcher narrowed the visible devices
-            device = local % ndev
+        if local >= ndev:
+            narrowed = [v for v in _VISIBLE_VARS
+                        if len([e for e in os.environ.get(v, "").split(",")
+                                if e.strip()]) == 1]
+            if ndev == 1 and narrowed:  # a launcher gave each rank one device
+                device = 0
+            else:  # two ranks on one device: RCCL refuses them; fail first
+                print("bench.py: rank %d (LOCAL_RANK %d) of %d needs device %d;"
+                      " %d visible" % (rank, local, world, local, ndev),
+                      file=sys.stderr)
+                sys.exit(3)
         rdzv = Rendezvous(rank, world)
         uid = rdzv.broadcast(Context.unique_id() if rank == 0 else None)
 
