@@ -96,7 +96,7 @@ $(SRC)/tensor_api.o: $(SRC)/tensor_api.cpp $(HDRS)
 # split8wp / split4p / split8wg / split128); loaded through XH_LIB_PATH only
 VDIR := build/variants
 VOBJS := $(patsubst %,$(VDIR)/%.o,$(VARIANT_KERNELS))
-$(VDIR)/%.o: $(SRC)/variants/%.hip $(HDRS)
+$(VDIR)/%.o: research/variants/%.hip $(HDRS)
 	@mkdir -p $(VDIR)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@
 $(VDIR)/train_select.o: $(SRC)/train_select.cpp $(HDRS)

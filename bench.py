@@ -67,6 +67,15 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
 KERNEL_OVERRIDES = ("XH_TRAIN_KERNEL", "XH_ROLLOUT_KERNEL", "XH_VALUE_KERNEL",
                     "XH_W0_FUSE")
 HBM_PEAK_GBS = 8000.0
+# the line's dtype names the arithmetic the train kernel ran (its `math`
+# from xh_trainer_kernel_info): f32 values on 16-bit matrix cores, exactly
+# split, f32 accumulation
+TRAIN_DTYPE = {
+    "f32_mfma": "f32",
+    "f16_pair_bf16_split": "f32 via f16-pair (layer 2, dH1) / 3-part bf16 "
+                           "split (dW2) MFMA, f32 accumulate",
+    "bf16_split": "f32 via 3-part bf16 split MFMA, f32 accumulate",
+}
 PHASE_ITERS = 3  # the phase-breakdown pass after the timed region
 
 
@@ -254,7 +263,8 @@ def env_only(args, cfg, ctx, rank, world, rdzv):
     env.synchronize()
     if rdzv:
         rdzv.barrier()
-    env.set_timing(True)
+    # the timed region carries no events; the per-launch HIP-event average
+    # comes from a second pass of the same launches after it
     t0 = time.perf_counter()
     for _ in range(args.steps):
         env.step(fetch=False)
@@ -264,6 +274,10 @@ def env_only(args, cfg, ctx, rank, world, rdzv):
     dt = time.perf_counter() - t0
     if rdzv:
         dt = rdzv.allreduce_max(dt)
+    env.set_timing(True)
+    for _ in range(args.steps):
+        env.step(fetch=False)
+    env.synchronize()
     ms, launches = env.kernel_time()
     env.set_timing(False)
     avg_ms = ms / max(launches, 1)
@@ -705,7 +719,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": TRAIN_DTYPE.get(kt["math"], "f32 (%s)" % kt["math"]),
         "data": "synthetic (fixed-size bin-packing instances, random-init "
                 "weights of the reference architecture)",
         "config": {"workload": workload + cfg["name"] % n + (

@@ -127,6 +127,9 @@ def _load():
                                    C.c_float, C.c_float, vp, vp, vp, vp, sz]),
         "xh_trainer_forget": (i, [vp]),
         "xh_trainer_set_record_last_step": (i, [vp, i]),
+        "xh_tensor_reduce": (i, [vp, i, vp, vp, C.c_float, sz, i,
+                                 C.POINTER(C.c_double),
+                                 C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -109,9 +109,16 @@ struct Part {
   long i;
 };
 
+// an empty max / argmax partial (no candidate element seen yet)
+constexpr long kNoIndex = 0x7fffffffffffffffL;
+
 __device__ __forceinline__ Part combine(int op, Part x, Part y) {
   if (op == kTensorMax || op == kTensorArgmax) {
-    // max_element keeps the first of equal maxima (tensor.cc:462-466)
+    // max_element keeps the first of equal maxima (tensor.cc:462-466); an
+    // empty side never wins, whatever its value (-inf elements are
+    // candidates like any other)
+    if (y.i == kNoIndex) return x;
+    if (x.i == kNoIndex) return y;
     if (y.v > x.v || (y.v == x.v && y.i < x.i)) return y;
     return x;
   }
@@ -145,7 +152,7 @@ __device__ __forceinline__ Part block_reduce(int op, Part p) {
 }
 
 __device__ __forceinline__ Part identity(int op) {
-  return (op == kTensorMax || op == kTensorArgmax) ? Part{-DBL_MAX, 0x7fffffffffffffffL}
+  return (op == kTensorMax || op == kTensorArgmax) ? Part{-DBL_MAX, kNoIndex}
                                                    : Part{0.0, 0};
 }
 
@@ -167,7 +174,10 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel(int op, const float *a
         q = Part{d * d, 0};
         break;
       }
-      default: q = Part{(double)x, i}; break;
+      // max_element's scan (`if (*largest < *it) largest = it`) never moves
+      // onto a NaN: NaN elements are no candidates (a NaN at index 0 is
+      // reduce_finish_kernel's case)
+      default: q = x != x ? identity(op) : Part{(double)x, i}; break;
     }
     p = combine(op, p, q);
   }
@@ -176,13 +186,22 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel(int op, const float *a
 }
 
 __global__ __launch_bounds__(kThreads) void reduce_finish_kernel(int op,
+                                                                 const float *a,
                                                                  const Part *part,
                                                                  int nparts,
                                                                  Part *out) {
   Part p = identity(op);
   for (int k = threadIdx.x; k < nparts; k += kThreads) p = combine(op, p, part[k]);
   p = block_reduce(op, p);
-  if (threadIdx.x == 0) *out = p;
+  if (threadIdx.x == 0) {
+    if (op == kTensorMax || op == kTensorArgmax) {
+      // max_element stays on element 0 when it is NaN (no element compares
+      // greater), and when every element is NaN: index 0, value a[0]
+      const float a0 = a[0];
+      if (a0 != a0 || p.i == kNoIndex) p = Part{(double)a0, 0};
+    }
+    *out = p;
+  }
 }
 
 // ------------------------------------------------------------- transpose --
@@ -251,8 +270,8 @@ hipError_t launch_tensor_reduce(int op, const float *a, const float *b, float s,
   Part *p = reinterpret_cast<Part *>(scratch);
   hipLaunchKernelGGL(reduce_kernel, dim3(parts), dim3(kThreads), 0, st, op, a, b,
                      s, n, p);
-  hipLaunchKernelGGL(reduce_finish_kernel, dim3(1), dim3(kThreads), 0, st, op, p,
-                     parts, p + parts);
+  hipLaunchKernelGGL(reduce_finish_kernel, dim3(1), dim3(kThreads), 0, st, op, a,
+                     p, parts, p + parts);
   return hipGetLastError();
 }
 

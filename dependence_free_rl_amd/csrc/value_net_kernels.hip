@@ -700,7 +700,8 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   o.b2 = a.params + o2 + V2;
   o.act0 = a.act[0];
   o.act1 = a.act[1];
-  o.act_rows = a.act_rows < 0 ? a.max_rows : a.act_rows;
+  // MlpArgs::act_rows (xh_kernels.h): 0 = every row, < 0 = none
+  o.act_rows = a.act_rows < 0 ? 0 : a.act_rows == 0 ? a.max_rows : a.act_rows;
   o.out = a.act[2];
   o.v_term = a.v_term && a.term_list ? a.v_term : nullptr;
   const int tiles = (a.max_rows + TM - 1) / TM;

@@ -181,7 +181,8 @@ struct xh_venv {
   // xh_venv_set_timing: HIP events around every step / apply / reset /
   // observe launch on the context's stream
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // recorded pairs
+  std::vector<hipEvent_t> event_pool;  // recycled by set_timing
 
   xh::VenvArgs args() const {
     xh::VenvArgs a{};
@@ -623,7 +624,8 @@ int do_rollout(xh_trainer *t) {
   // diagnostics only (tests, health checks): off in the product path
   a.logits_out = t->cfg.record_last_step ? t->logits : nullptr;
   a.probs_out = t->cfg.record_last_step ? t->probs : nullptr;
-  if (t->cfg.record_last_step) t->last_step_recorded = true;
+  // cleared as well: a rollout without recording leaves no current logits
+  t->last_step_recorded = t->cfg.record_last_step != 0;
   CHK(timed(t, "rollout_step", [&]() {
     return xh::launch_rollout_step(a, t->cfg.policy_h1, t->cfg.policy_h2,
                                    t->rgrid, s, &t->last_rollout);
@@ -2051,7 +2053,7 @@ int xh_trainer_set_env_state(xh_trainer *t, int first, int count,
 // ------------------------------------------------------------------ venv --
 }  // extern "C"
 namespace {
-void venv_drop_events(xh_venv *v);
+void venv_drop_events(xh_venv *v, bool destroy = false);
 }  // namespace
 extern "C" {
 
@@ -2119,7 +2121,7 @@ int xh_venv_destroy(xh_venv *v) {
     if (!v) return XH_OK;
     (void)hipSetDevice(v->ctx->device);
     (void)hipStreamSynchronize(v->ctx->stream);
-    venv_drop_events(v);
+    venv_drop_events(v, true);
     for (void *p : v->buf)
       if (p) (void)hipFree(p);
     if (v->err) (void)hipFree(v->err);
@@ -2160,25 +2162,49 @@ int venv_launch(xh_venv *v, int op, int mode, bool use_mask, bool obs) {
   a.obs = obs ? (float *)v->buf[XH_VENV_OBS] : nullptr;
   if (op == xh::kVenvObserve) a.obs = (float *)v->buf[XH_VENV_OBS];
   if (mode == 0) a.reward = nullptr;
+  // events from a pool (no creation per launch); a pair is kept only once
+  // both of its records are on the stream, so a failed launch leaves no
+  // half-recorded pair behind
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  auto pooled = [&](hipEvent_t *e) -> hipError_t {
+    if (!v->event_pool.empty()) {
+      *e = v->event_pool.back();
+      v->event_pool.pop_back();
+      return hipSuccess;
+    }
+    return hipEventCreateWithFlags(e, hipEventDisableSystemFence);
+  };
   if (v->timing) {
-    HIPCHK(hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence));
-    HIPCHK(hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence));
-    v->events.push_back(ev);
+    HIPCHK(pooled(&ev.first));
+    HIPCHK(pooled(&ev.second));
     HIPCHK(hipEventRecord(ev.first, v->ctx->stream));
   }
   const hipError_t e = xh::launch_venv(a, op, v->ctx->stream);
-  if (e != hipSuccess)
+  if (e != hipSuccess) {
+    if (v->timing) {
+      v->event_pool.push_back(ev.first);
+      v->event_pool.push_back(ev.second);
+    }
     return fail(XH_ERR_HIP, "venv launch: %s", hipGetErrorString(e));
-  if (v->timing) HIPCHK(hipEventRecord(ev.second, v->ctx->stream));
+  }
+  if (v->timing) {
+    HIPCHK(hipEventRecord(ev.second, v->ctx->stream));
+    v->events.push_back(ev);
+  }
   return XH_OK;
 }
-void venv_drop_events(xh_venv *v) {
+// the recorded pairs back into the pool (the stream is synchronised first);
+// destroy = true at xh_venv_destroy
+void venv_drop_events(xh_venv *v, bool destroy) {
   for (auto &ev : v->events) {
-    (void)hipEventDestroy(ev.first);
-    (void)hipEventDestroy(ev.second);
+    v->event_pool.push_back(ev.first);
+    v->event_pool.push_back(ev.second);
   }
   v->events.clear();
+  if (destroy) {
+    for (hipEvent_t e : v->event_pool) (void)hipEventDestroy(e);
+    v->event_pool.clear();
+  }
 }
 }  // namespace
 

@@ -1,5 +1,6 @@
 // xylo/rl.h (xylo-hip drop-in layer): actions (discrete_action with its loss
-// gradients, continuous_action), trajectories, replay buffer (sample_td,
+// gradients; the reference's continuous_action, rl.h:77-109, is not carried:
+// no bin-packing app or learner on this path uses it), trajectories, replay buffer (sample_td,
 // sample_transitions, forget), environment / policy / agent / learner
 // interfaces (rl.h:17-392), same names and signatures.
 //
@@ -94,38 +95,6 @@ template <std::size_t range> struct discrete_action {
         std::min(clipped_ratio * advantage, ratio * advantage) * -1;
     output[choice] = importance_grad / input[choice];
   }
-};
-
-// rl.h:77-109: a Gaussian action with a learned mean (host arithmetic; no
-// device learner uses it).
-struct continuous_action {
-  static std::size_t cardinality() { return 1; }
-
-  float action = 0;
-  float mean = 0;
-  float stddev = 1;
-
-  void from_vector(vector_view a) {
-    vector result({1});
-    mean = a[0];
-    normal_distribution(mean, stddev, result);
-    action = result[0];
-  }
-  void gradient_log(vector_view input, vector_view output, float reward,
-                    float o_value) const {
-    if (input.size() != 1 || output.size() != 1) throw std::exception();
-    float log_action_grad = (action - input[0]) / (stddev * stddev);
-    float weighted_grad = log_action_grad * (reward / o_value - 1) * -1;
-    float normalized_input_action_diff = (action - input[0]) / stddev;
-    float normalized_action_diff = (action - mean) / stddev;
-    float importance_grad =
-        ::exp(-0.5 *
-              (normalized_input_action_diff * normalized_input_action_diff -
-               normalized_action_diff * normalized_action_diff)) *
-        weighted_grad;
-    output[0] = importance_grad;
-  }
-  void clipped_gradient(vector_view, vector_view, float, float) const {}
 };
 
 template <typename A, typename S> struct transition {

@@ -142,18 +142,21 @@ def test_c3_full_size_sampling_vs_oracle(ctx, off):
     job against the oracle's sequential reference-order sampler
     (discrete_distribution on the model's probabilities, rl.h:27-30,
     tensor.cc:467-470) on the same streams.  Actions, states and dones match
-    bit for bit, p_old within 1e-4; an env whose sampled bin differs (a
-    near-tie of a cumulative probability, resolved differently by the f16-pair
-    layer 2 and the oracle's double sums) diverges from there on and is
-    counted: at most one of the 256 envs."""
+    bit for bit, p_old within 1e-4.  An env whose sampled bin differs
+    diverges from there on; it is allowed only as a PROVEN near-tie: at its
+    first differing step (same state on both sides) the draw u, recomputed
+    from the env's reference-order stream position, lies between the
+    oracle's and the device's cumulative probability at the boundary they
+    resolve differently, and those two differ by at most TIE_TOL = 1e-4 (the
+    stated probability tolerance p_old is held to).  Anything else fails."""
     from oracle import pyoracle as po
     from dependence_free_rl_amd import POLICY, VALUE, Trainer, init_policy, init_value
     from dependence_free_rl_amd.trainer import (BUF_ACTION, BUF_BINS, BUF_DONE,
-                                                BUF_POLD)
+                                                BUF_POLD, BUF_QOLD)
     N, S, B, D, T, x0 = 32768, 256, 64, 2, 4, 1357911
     pp, vp = init_policy(D, 128, 128, seed=51), init_value(B, D, seed=52)
     tr = Trainer(ctx, bins=B, dims=D, num_envs=N, steps=T, widths=(128, 128),
-                 rng_state=x0)
+                 rng_state=x0, record_distrib=True)
     tr.set_params(POLICY, pp)
     tr.set_params(VALUE, vp)
     tr.rollout()
@@ -162,6 +165,7 @@ def test_c3_full_size_sampling_vs_oracle(ctx, off):
     bins = tr.buffer(BUF_BINS)[:T, off:off + S]
     done = tr.buffer(BUF_DONE)[:, off:off + S]
     pold = tr.buffer(BUF_POLD)[:, off:off + S]
+    q = tr.buffer(BUF_QOLD)[:, off:off + S]  # every sampled distribution
     tr.close()
     # the oracle sample: env i constructed at engine position 2 (off + i),
     # its step draws from 2 N + 4 T (off + i) on
@@ -178,12 +182,19 @@ def test_c3_full_size_sampling_vs_oracle(ctx, off):
     o_pold = orc.buf(po.BUF_STEP_PCHOICE).reshape(S, T).T
     diff = act != o_act
     bad = diff.any(0)
+    o_item = orc.buf(po.BUF_STEP_ITEM).reshape(S, T, -1).swapaxes(0, 1)
+    from sampling_ties import near_tie
+    ties = [near_tie(po, pp, B, D, N, T, x0, off + i, t, o_bins[t, i],
+                      o_item[t, i], q[t, i], int(act[t, i]), int(o_act[t, i]))
+            for i in np.flatnonzero(bad)
+            for t in [int(np.flatnonzero(diff[:, i])[0])]]
     rec = {"test": "c3_full_size_vs_oracle", "offset": off, "envs": S,
            "actions": int(act.size), "differ": int(diff.sum()),
-           "envs_differ": int(bad.sum())}
+           "envs_differ": int(bad.sum()), "near_ties": ties}
     print(rec)
     log_record("sampling_agreement.jsonl", rec)
-    assert bad.sum() <= 1, rec
+    for tie in ties:
+        assert tie["proven"], rec
     ok = ~bad
     np.testing.assert_array_equal(act[:, ok], o_act[:, ok])
     np.testing.assert_array_equal(bins[:, ok], o_bins[:, ok])
