@@ -136,7 +136,8 @@ def cpu_baseline():
     if B == 64 and D == 2 and os.path.exists(bp64):
         harness, env_src = bp64, "bp::environment (bin_packing.h, num_bins = 64)"
     n_env, iters = 16, max(1, REF_ITERS // 3)
-    learner = "ppo_learner" if ALGO == "ppo" else "actor_critic_learner"
+    learner = {"ppo": "ppo_learner", "klppo": "kl_ppo_learner (ppo2_training.cc)",
+               "ac": "actor_critic_learner"}[ALGO]
     sample = ("reference %s on %s, %d envs x T=%d x %d iterations per "
               "process, B=%d D=%d [%d,%d], single-threaded processes" % (
                   learner, env_src, n_env, T, iters, B, D, H1, H2))
@@ -172,9 +173,10 @@ def cpu_baseline():
     from dependence_free_rl_amd.trainer import init_policy, init_value
     n_env, iters = 8, 3
     pol = po.perbin_model(F0, [H1, H2],
-                          po.OR_SOFTMAX if ALGO == "ppo" else po.OR_SOFTMAX_XENT)
+                          po.OR_SOFTMAX_XENT if ALGO == "ac" else po.OR_SOFTMAX)
     val = po.full_model(B * F0, [V1, V2], 1)
-    tr = po.Trainer(po.OR_PPO if ALGO == "ppo" else po.OR_AC, B, D, n_env, T,
+    tr = po.Trainer({"ppo": po.OR_PPO, "klppo": po.OR_KLPPO, "ac": po.OR_AC}[ALGO],
+                    B, D, n_env, T,
                     pol, init_policy(D, H1, H2),
                     val, init_value(B, D), x0=1)
     t0 = time.perf_counter()
@@ -184,7 +186,7 @@ def cpu_baseline():
     dt = time.perf_counter() - t0
     return {"value": round(n_env * T * iters / dt, 3), "unit": "env-steps/s",
             "cores": 1, "kind": "port",
-            "sample": "oracle port, %d envs x T=%d x %d iterations" % (
+            "sample": "oracle port (%s), %d envs x T=%d x %d iterations" % (ALGO,
                 n_env, T, iters)}
 
 
@@ -514,11 +516,6 @@ def main():
     if args.algo:
         global ALGO
         ALGO = args.algo
-        if ALGO == "klppo" and not args.no_cpu_baseline:
-            print("bench.py: no CPU baseline for --algo klppo (the harness "
-                  "times ppo / actor-critic learners); pass --no-cpu-baseline",
-                  file=sys.stderr)
-            sys.exit(2)
     if args.rollout_steps:
         global T
         T = args.rollout_steps

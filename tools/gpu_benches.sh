@@ -15,7 +15,7 @@ done
 timeout -k 10 300 python -u bench.py --rollout-steps 32 --steps 3 --warmup 1 --no-cpu-baseline > $O/bT32.log 2>&1 || { tail -5 $O/bT32.log; exit 1; }
 tail -1 $O/bT32.log > $O/profiles/${TAG}_bench_config3_T32.json
 for c in 3 2 5; do
-  timeout -k 10 300 python -u bench.py --config $c --algo klppo --steps 5 --warmup 1 --no-cpu-baseline > $O/bkl$c.log 2>&1 || { tail -5 $O/bkl$c.log; exit 1; }
+  timeout -k 10 300 python -u bench.py --config $c --algo klppo --steps 5 --warmup 1 > $O/bkl$c.log 2>&1 || { tail -5 $O/bkl$c.log; exit 1; }
   tail -1 $O/bkl$c.log > $O/profiles/${TAG}_bench_config${c}_klppo.json
 done
 cut -c1-200 $O/profiles/${TAG}_bench_config*.json
