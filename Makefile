@@ -13,7 +13,7 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/env_kernels.o $(SRC)/kl_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/value_net_kernels.o \
-            $(SRC)/policy_spec8_kernels.o \
+            $(SRC)/policy_spec8_kernels.o $(SRC)/policy_spec8_kl_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \
             $(SRC)/policy_split4h_kernels.o $(SRC)/policy_split4h_kl_kernels.o \
@@ -75,6 +75,8 @@ $(SRC)/policy_split8wh_kl_kernels.o: $(SRC)/policy_split8wh_kernels.hip $(HDRS)
 $(SRC)/policy_split8x_kl_kernels.o: $(SRC)/policy_split8x_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_policy_split8x_kernels) -DXH_8X_KL_TU=1 \
 	    -mllvm -pragma-unroll-threshold=200000 -c $< -o $@
+$(SRC)/policy_spec8_kl_kernels.o: $(SRC)/policy_spec8_kernels.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(FLAGS_policy_spec8_kernels) -DXH_SP8_KL_TU=1 -c $< -o $@
 $(SRC)/policy_split4h_kl_kernels.o: $(SRC)/policy_split4h_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_policy_split4h_kernels) -DXH_4H_KL_TU=1 \
 	    -mllvm -pragma-unroll-threshold=200000 -c $< -o $@

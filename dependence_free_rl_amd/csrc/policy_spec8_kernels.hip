@@ -84,6 +84,25 @@
 #ifndef XH_SP8_VFIRST
 #define XH_SP8_VFIRST 1
 #endif
+// XH_SP8_KL_TU=1 (policy_spec8_kl_kernels.o): the KL-PPO build,
+// policy_train_spec8_kl_kernel -- kl_ppo_learner's epoch
+// (policy_gradient.h:310-335) over every row of its state matrix as
+// policy_train_split8wh_kl_kernel: the T N transitions, the open
+// trajectories' end rows (slot T, q of step T - 1, valid unless step T - 1
+// ended), the terminal end rows E_t of end_list (the chosen bin with the
+// item taken back out, rl.h:336-343); end rows carry A = 0; the loss head is
+// kl_regulated_loss (policy_gradient.h:41-85) through softmax_layer::backward
+// (nn.h:393-417), and each workgroup sums KL(q || p) over its valid rows into
+// kl_part.  Preprocessor blocks, so the PPO object compiles from exactly its
+// measured source.
+#ifndef XH_SP8_KL_TU
+#define XH_SP8_KL_TU 0
+#endif
+#if XH_SP8_KL_TU
+#define SP8KL(...) __VA_ARGS__
+#else
+#define SP8KL(...)
+#endif
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
 #endif
@@ -123,7 +142,12 @@ constexpr int F_SC = F_REC + 16;   // [16] scale reduction scratch, the scales
 constexpr int F_B3 = F_SC + 16;    // [4]
 constexpr int F_DB3 = F_B3 + 4;    // [32] matrix wave 0's db3 sums, per lane
 constexpr int F_SIMD = F_DB3 + 32; // [8] the SIMD each wave runs on (ints)
+#if XH_SP8_KL_TU
+constexpr int F_Q = F_SIMD + 8;    // [4 slots][64 bins] old distribution q
+constexpr int F_END = F_Q + 256;
+#else
 constexpr int F_END = F_SIMD + 8;
+#endif
 constexpr size_t kLds = L_F + sizeof(float) * F_END;
 static_assert(kLds <= 160 * 1024, "LDS");
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -182,7 +206,11 @@ __device__ __forceinline__ float add_halves(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+#if XH_SP8_KL_TU
+__global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kl_kernel(PolicyTrainArgs a) {
+#else
 __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyTrainArgs a) {
+#endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float *lf = reinterpret_cast<float *>(lds + L_F);
   const PolicyLayout PL{kF0, kH, kH};
@@ -190,7 +218,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int l = tid & 63, h = l >> 5, l31 = l & 31;
+#if XH_SP8_KL_TU
+  const int NT = a.b.T * a.b.N;
+  const int n_end = *a.n_end;
+  const int ngroups = NT + a.b.N + n_end;
+  const float beta = *a.beta;
+#else
   const int ngroups = a.b.T * a.b.N;
+#endif
   // this workgroup's groups g_j = b0 + j gridDim.x, j < J (XCD-aware b0 as
   // policy_train_split8wh_kernel); look-ahead indices past the end are
   // clamped to the last group and their results discarded
@@ -345,8 +380,35 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // wave 0 stages the rows of a group: raw loads (the row's two bins per
     // lane; lanes 0-2 the action, old probability, advantage, lanes 3.. the
     // item's first coordinates), the stores into an LDS slot a phase later
+#if XH_SP8_KL_TU
+    // the row of the [T+1][N] arrays group g reads and the row of its old
+    // distribution (kind 0 transition, 1 open end row, 2 terminal end row);
+    // g is wave-uniform: scalar branches, and only terminal end rows wait for
+    // their end_list entry
+    auto kl_rows = [&](int g, size_t &ti, size_t &qi) {
+      const int N = a.b.N;
+      g = __builtin_amdgcn_readfirstlane(g);
+      if (g < NT) {
+        ti = qi = (size_t)g;
+      } else if (g < NT + N) {
+        ti = (size_t)NT + (g - NT);
+        qi = (size_t)(NT - N) + (g - NT);
+      } else {
+        const int jj = min(g - NT - N, max(n_end - 1, 0));
+        const int te = __builtin_amdgcn_readfirstlane(a.end_list[jj]);
+        ti = qi = (size_t)te;
+      }
+    };
+#endif
     auto stage_load = [&](int j) {
+#if XH_SP8_KL_TU
+      size_t ti = tindex(j), qi = 0;
+      kl_rows((int)ti, ti, qi);
+      const size_t ri = qi;  // (open end rows: their record values are unused)
+#else
       const size_t ti = tindex(j);
+      const size_t ri = ti;
+#endif
       // the row's bins: a wave-uniform base and the lane id recomputed
       // (mbcnt), not a per-lane pointer held (or spilled) across the loop
       const int lane =
@@ -354,23 +416,65 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       const unsigned short *rowp =
           reinterpret_cast<const unsigned short *>(a.b.bins + ti * (kB * kD));
       const int bins = rowp[lane];
-      const unsigned long long p0 = (unsigned long long)(a.b.action + ti);
-      const unsigned long long p1 = (unsigned long long)(a.b.pold + ti);
-      const unsigned long long p2 = (unsigned long long)(a.adv + ti);
+      const unsigned long long p0 = (unsigned long long)(a.b.action + ri);
+#if XH_SP8_KL_TU
+      // lane 1: the aligned word holding done[qi] (an open end row's validity)
+      const unsigned long long p1 = (unsigned long long)(a.b.done + (qi & ~(size_t)3));
+#else
+      const unsigned long long p1 = (unsigned long long)(a.b.pold + ri);
+#endif
+      const unsigned long long p2 = (unsigned long long)(a.adv + ri);
       const unsigned long long p3 = (unsigned long long)(a.b.items + ti * 4);
       unsigned long long pa = l >= 3 ? p3 : p2;
       pa = l == 1 ? p1 : pa;
       pa = l == 0 ? p0 : pa;
+#if XH_SP8_KL_TU
+      // the old distribution straight into its LDS slot (j & 3; its group
+      // j - 4 finished with it a period ago), waited for at stage_store
+      typedef __attribute__((address_space(1))) void gvoid;
+      typedef __attribute__((address_space(3))) void lvoid;
+      __builtin_amdgcn_global_load_lds((gvoid *)(a.qold + qi * kB + l),
+                                       (lvoid *)(lf + F_Q + (j & 3) * 64), 4, 0, 0);
+#endif
       return Raw{bins, *reinterpret_cast<const int *>(pa)};
     };
-    auto stage_store = [&](const Raw &r, int sl) {
+    auto stage_store = [&](const Raw &r, int sl SP8KL(, int j)) {
+#if XH_SP8_KL_TU
+      const int g = __builtin_amdgcn_readfirstlane((int)tindex(j));
+      const int kind = g < NT ? 0 : g < NT + a.b.N ? 1 : 2;
+      // the terminal view: the chosen bin without the item (rl.h:336-343)
+      const int itm = __builtin_amdgcn_readlane(r.rec, 3);
+      const bool sub = kind == 2 && l == __builtin_amdgcn_readfirstlane(r.rec);
+      const float x0 =
+          (float)((signed char)(r.bi & 0xff) - (sub ? (signed char)(itm & 0xff) : 0)) /
+          (float)kCapacity;
+      const float x1 =
+          (float)((signed char)((r.bi >> 8) & 0xff) - (sub ? (signed char)((itm >> 8) & 0xff) : 0)) /
+          (float)kCapacity;
+      // the old distribution's LDS-direct load (issued with this group's
+      // staging loads, a phase ago): complete before the phase's barrier
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
       const float x0 = (float)(signed char)(r.bi & 0xff) / (float)kCapacity;
       const float x1 = (float)(signed char)((r.bi >> 8) & 0xff) / (float)kCapacity;
+#endif
       lf[F_X + sl * 128 + l] = x0;
       lf[F_X + sl * 128 + 64 + l] = x1;
       const int item = __builtin_amdgcn_readlane(r.rec, 3);
       const int i0 = (signed char)(item & 0xff), i1 = (signed char)((item >> 8) & 0xff);
+#if XH_SP8_KL_TU
+      // the record: action (lane 0), whether the row counts (lane 1: not a
+      // terminal row past n_end, nor an open end row whose env ended at step
+      // T - 1), advantage (lane 2, 0 for end rows)
+      const int dw = __builtin_amdgcn_readlane(r.rec, 1);
+      const size_t qi1 = kind == 1 ? (size_t)(NT - a.b.N) + (g - NT) : 0;
+      const int ended = (dw >> (8 * (int)(qi1 & 3))) & 0xff;
+      const bool valid = kind == 0 || (kind == 1 ? ended == 0 : g - NT - a.b.N < n_end);
+      if (l == 0 || l == 2) lf[F_REC + 4 * sl + l] = kind == 0 ? __int_as_float(r.rec) : 0.0f;
+      if (l == 1) lf[F_REC + 4 * sl + 1] = valid ? 1.0f : 0.0f;
+#else
       if (l < 3) lf[F_REC + 4 * sl + l] = __int_as_float(r.rec);
+#endif
       if (l == 3)
         lf[F_REC + 4 * sl + 3] =
             (i0 == a.env.item_a[0] && i1 == a.env.item_a[1]) ? 1.0f : 0.0f;
@@ -453,7 +557,14 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       float b3, ex0, ex1, se, p0, p1, gc, pc;
       int cu;
       float po, Ac;  // the record, wave-uniform from stage 1 on
+#if XH_SP8_KL_TU
+      float q0, q1;  // the old distribution of rows l31, 32 + l31 (pc, gc:
+                     // the probability-space gradients; po: the row counts)
+#endif
     } sm;
+#if XH_SP8_KL_TU
+    double kl_acc = 0.0;  // KL(q || p) of the valid rows this wave summed
+#endif
     auto softmax_stage = [&](int gi, int gpar, bool acc, int stage) {
       const int rs = gi & 3;
       switch (stage) {
@@ -462,6 +573,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           sm.b3 = lf[F_B3];
           sm.z0 = lds4v(lf + F_Z + 4 * l31);
           sm.z1 = lds4v(lf + F_Z + 4 * (32 + l31));
+#if XH_SP8_KL_TU
+          sm.q0 = lf[F_Q + 64 * rs + l31];
+          sm.q1 = lf[F_Q + 64 * rs + 32 + l31];
+#endif
           if (s == 0) {
             // (wave 0's per-lane addresses recomputed here: held across the
             // loop they spilled)
@@ -488,6 +603,37 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           sm.p1 = sm.ex1 * rse;
           break;
         }
+#if XH_SP8_KL_TU
+        case 4: {
+          // kl_regulated_loss (policy_gradient.h:41-85): softmax_gradient_log
+          // + beta (p - q) as a probability-space gradient (softmax_layer::
+          // backward in the next two stages); the KL sum by one matrix wave
+          // per group, in turn, lane half 0 (both halves hold the rows)
+          const int cu = sm.cu;
+          const float Ac = sm.Ac;
+          float g0 = fmaf(beta, sm.p0 - sm.q0, sm.p0 * Ac);
+          float g1 = fmaf(beta, sm.p1 - sm.q1, sm.p1 * Ac);
+          if (l31 == cu) g0 -= Ac;
+          if (32 + l31 == cu) g1 -= Ac;
+          sm.pc = g0;
+          sm.gc = g1;
+          const bool vld = __float_as_int(sm.po) != 0;
+          if (vld && (gi & 3) == s && h == 0)
+            kl_acc += (double)(sm.q0 * logf(sm.q0 / sm.p0)) +
+                      (double)(sm.q1 * logf(sm.q1 / sm.p1));
+          break;
+        }
+        case 5:
+          sm.se = half_sum32(sm.p0 * sm.pc + sm.p1 * sm.gc);
+          break;
+        case 6: {
+          const float sgv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm.se), 31));
+          const bool vld = __float_as_int(sm.po) != 0;
+          gz[0] = vld ? sm.p0 * (sm.pc - sgv) : 0.0f;
+          gz[1] = vld ? sm.p1 * (sm.gc - sgv) : 0.0f;
+          break;
+        }
+#else
         case 4: {
           const int cu = sm.cu;
           sm.pc = __int_as_float(
@@ -519,6 +665,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           }
           break;
         }
+#endif
         default:
           if (s == 0 && h == 0) {
             const int lo = opaque(l31);
@@ -607,7 +754,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     auto b_task = [&](const f32x16s (&c)[2], int gi, int gpar, bool acc, int k) {
       if (k == 0)
         softmax_stage(gi, gpar, acc, 0);
-      else if (k >= 3 && k < 9)
+      else if (k >= 3 && k < (XH_SP8_KL_TU ? 10 : 9))
         softmax_stage(gi, gpar, acc, k - 2);
       else if (k >= 12 && k < 44) {
         dw3_e(c, (k - 12) >> 4, (k - 12) & 15);
@@ -620,9 +767,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     if (XH_SP8_PRIO & 3) __builtin_amdgcn_s_setprio(XH_SP8_PRIO & 3);
     f32x16s c[2];
     if (s == 0) {
-      stage_store(stage_load(0), 0);
-      stage_store(stage_load(1), 1);
-      stage_store(stage_load(2), 2);
+      stage_store(stage_load(0), 0 SP8KL(, 0));
+      stage_store(stage_load(1), 1 SP8KL(, 1));
+      stage_store(stage_load(2), 2 SP8KL(, 2));
     }
     __syncthreads();  // P1: rows staged          (vector: L1(0))
     __syncthreads();  // P2
@@ -651,7 +798,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       __syncthreads();
       // B(j): dW2 of group j with group j+1's softmax, dW3 / db2 sums and
       // masks in its MFMA slots
-      if (s == 0) stage_store(raw, (j + 3) & 3);
+      if (s == 0) stage_store(raw, (j + 3) & 3 SP8KL(, j + 3));
       const bool acc = j + 1 < J;
       if (SP8_RUN(1 | 16))
         dw2(par, [&](int k) { b_task(c, j + 1, 1 - par, acc, k); });
@@ -662,6 +809,20 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       if (j + 1 < J) period(j + 1, Par<1>{});
     }
 
+#if XH_SP8_KL_TU
+    {
+      // the workgroup's KL sum: the matrix waves' doubles in a fixed order
+      // (the loop's last barrier is behind: F_Z is free; the vector waves
+      // meet this barrier after their loop)
+      double v = kl_acc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+      double *kd = reinterpret_cast<double *>(lf + F_Z);
+      if (l == 0) kd[s] = v;
+      __syncthreads();
+      if (s == 0 && l == 0) a.kl_part[blockIdx.x] = (kd[0] + kd[1]) + (kd[2] + kd[3]);
+    }
+#endif
     // ---- write-out (every entry has exactly one producing lane)
     const float rSH = 0.5f / SH;  // (the masks were 2.0)
 #pragma unroll
@@ -975,6 +1136,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       if (j + 1 < J) period(j + 1, Par<1>{});
     }
 
+#if XH_SP8_KL_TU
+    __syncthreads();  // the matrix waves' KL sum
+#endif
     // ---- write-out: dW1 / db1 of feature fi (the two lane halves hold row
     // subsets; dH1 was in units of S_D)
     float tw0 = w0 + __shfl_xor(w0, 32, kWave);
@@ -1001,6 +1165,19 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
 
 }  // namespace sp8
 
+#if XH_SP8_KL_TU
+hipError_t launch_policy_train_spec8_kl(const PolicyTrainArgs &a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)sp8::policy_train_spec8_kl_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sp8::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(sp8::policy_train_spec8_kl_kernel, dim3(grid), dim3(sp8::kThreads),
+                     sp8::kLds, s, a);
+  return hipGetLastError();
+}
+#else
 hipError_t launch_policy_train_spec8(const PolicyTrainArgs &a, int grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
@@ -1012,5 +1189,6 @@ hipError_t launch_policy_train_spec8(const PolicyTrainArgs &a, int grid, hipStre
                      sp8::kLds, s, a);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace xh

@@ -3,7 +3,7 @@
 // Product kernels (libxylo_hip.so), f16 pairs + the exact bf16 split
 // (DESIGN.md §3.0a-d):
 //   64 bins, 2-D, [128,128] (configs 3 / 4)  policy_train_spec8_kernel
-//                                  (KL-PPO: policy_train_split8wh_kl_kernel;
+//                                  (KL-PPO: policy_train_spec8_kl_kernel;
 //                                  XH_TRAIN_KERNEL=split8wh: the earlier
 //                                  policy_train_split8wh_kernel)
 //   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
@@ -92,12 +92,14 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
     }
 #endif
   } else {
-    // the wave-specialised kernel for PPO / actor-critic; the KL-PPO build
-    // and the override XH_TRAIN_KERNEL=split8wh (A/B runs, the test of the
-    // two against each other) run policy_train_split8wh_kernel
-    if (!ov && a.algo != kKLPPO) {
-      info->name = "policy_train_spec8_kernel";
-      return launch_policy_train_spec8(a, grid, s);
+    // the wave-specialised kernel (PPO / actor-critic) and its KL-PPO build;
+    // the override XH_TRAIN_KERNEL=split8wh (A/B runs, the test of the two
+    // against each other) runs policy_train_split8wh_kernel / its KL build
+    if (!ov) {
+      info->name = a.algo == kKLPPO ? "policy_train_spec8_kl_kernel"
+                                    : "policy_train_spec8_kernel";
+      return a.algo == kKLPPO ? launch_policy_train_spec8_kl(a, grid, s)
+                              : launch_policy_train_spec8(a, grid, s);
     }
     if (!ov || std::strcmp(ov, "split8wh") == 0) {
       info->name = a.algo == kKLPPO ? "policy_train_split8wh_kl_kernel"

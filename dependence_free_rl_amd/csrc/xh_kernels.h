@@ -396,6 +396,8 @@ hipError_t launch_policy_train_split8wh_kl(const PolicyTrainArgs &a, int grid,
                                            hipStream_t s);
 // the wave-specialised config-3 / config-4 epoch (policy_spec8_kernels.hip)
 hipError_t launch_policy_train_spec8(const PolicyTrainArgs &a, int grid, hipStream_t s);
+// its KL-PPO build (policy_spec8_kl_kernels.o)
+hipError_t launch_policy_train_spec8_kl(const PolicyTrainArgs &a, int grid, hipStream_t s);
 hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,

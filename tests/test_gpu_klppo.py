@@ -5,8 +5,9 @@ every row of its state matrix: the transitions, the open trajectories' end
 rows and the terminal end rows (rl.h:336-343), with kl_regulated_loss
 (policy_gradient.h:41-85) and beta adapted between epochs from the mean KL.
 At the 64-bin 2-D [128,128] shape (BASELINE config 3's) the epoch runs
-policy_train_split8wh_kl_kernel, the KL-PPO build of the headline train
-kernel, at the 128-bin 3-D shape (config 5's) policy_train_split8x_kl_kernel
+policy_train_spec8_kl_kernel, the KL-PPO build of the wave-specialised
+headline train kernel (its round-4 predecessor policy_train_split8wh_kl_kernel
+under XH_TRAIN_KERNEL=split8wh), at the 128-bin 3-D shape (config 5's) policy_train_split8x_kl_kernel
 and at the 32-bin 1-D [64,64] shape (config 2's, two rows per 64-row group)
 policy_train_split4h_kl_kernel (f16 pairs + the exact bf16 split, DESIGN.md
 §3.0a-d).  Lockstep iterations: the oracle learns from the
@@ -25,17 +26,17 @@ from gpu_helpers import step_major
 
 pytestmark = pytest.mark.gpu
 
-KL_KERNEL = {64: "policy_train_split8wh_kl_kernel", 128: "policy_train_split8x_kl_kernel",
+KL_KERNEL = {64: "policy_train_spec8_kl_kernel", 128: "policy_train_split8x_kl_kernel",
              32: "policy_train_split4h_kl_kernel"}
 
 
 @pytest.mark.parametrize("B,D,N,T,iters,cap,kernel",
                          [(64, 2, 48, 4, 5, 0, "split"), (64, 2, 32, 4, 4, 1, "split"),
-                          (64, 2, 48, 4, 5, 0, "f32"),
+                          (64, 2, 48, 4, 5, 0, "f32"), (64, 2, 48, 4, 5, 0, "split8wh"),
                           (128, 3, 24, 8, 5, 0, "split"), (128, 3, 24, 8, 5, 1, "split"),
                           (32, 1, 64, 4, 5, 0, "split"), (32, 1, 48, 4, 5, 1, "split"),
                           (32, 1, 64, 4, 5, 0, "f32")],
-                         ids=["b64_n48", "b64_n32_cap1", "b64_n48_f32", "b128_n24",
+                         ids=["b64_n48", "b64_n32_cap1", "b64_n48_f32", "b64_n48_8wh", "b128_n24",
                               "b128_n24_cap1", "b32_n64", "b32_n48_cap1", "b32_n64_f32"])
 def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, kernel):
     """kernel "f32": the same iterations on the f32-MFMA KL kernel
@@ -49,6 +50,9 @@ def test_klppo_split_matches_oracle(ctx, monkeypatch, B, D, N, T, iters, cap, ke
     if kernel == "f32":
         monkeypatch.setenv("XH_TRAIN_KERNEL", "f32")
         want = "policy_train_kernel<kl>"
+    elif kernel == "split8wh":  # the round-4 KL build, kept for A/B
+        monkeypatch.setenv("XH_TRAIN_KERNEL", "split8wh")
+        want = "policy_train_split8wh_kl_kernel"
     pp, vp = init_policy(D, *widths, seed=61), init_value(B, D, seed=62)
     tr = Trainer(ctx, algo="klppo", bins=B, dims=D, num_envs=N, steps=T,
                  widths=widths, rng_state=x0, wd_policy=wd, train_grid_cap=cap)
