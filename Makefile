@@ -14,6 +14,7 @@ OBJS     := $(SRC)/policy_kernels.o $(SRC)/value_kernels.o \
             $(SRC)/heuristic_kernels.o $(SRC)/dense_kernels.o \
             $(SRC)/pg_kernels.o $(SRC)/venv_kernels.o $(SRC)/value_net_kernels.o \
             $(SRC)/policy_spec8_kernels.o $(SRC)/policy_spec8_kl_kernels.o \
+            $(SRC)/policy_spec4_kernels.o \
             $(SRC)/policy_split8wh_kernels.o $(SRC)/policy_split8wh_kl_kernels.o \
             $(SRC)/policy_split8x_kernels.o $(SRC)/policy_split8x_kl_kernels.o \
             $(SRC)/policy_split4h_kernels.o $(SRC)/policy_split4h_kl_kernels.o \
@@ -62,6 +63,7 @@ FLAGS_policy_split8x_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split4h_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_split8wg_kernels := -mllvm -amdgpu-mfma-vgpr-form
 FLAGS_policy_spec8_kernels := -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize
+FLAGS_policy_spec4_kernels := -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c $< -o $@

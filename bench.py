@@ -202,7 +202,8 @@ def library_sha256():
     return h.hexdigest()
 
 
-def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None):
+def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None,
+                meta_match=None):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 FETCH_SIZE /
     WRITE_SIZE summary (separate --pmc passes; tools/pmc_summary.py):
     2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read correction measured for 1- to
@@ -222,6 +223,8 @@ def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None):
             summ = json.load(f)
         meta = summ.get("_meta", {})
         if lib_sha is None or meta.get("library_sha256") != lib_sha:
+            continue
+        if meta_match and any(meta.get(k) != v for k, v in meta_match.items()):
             continue
         # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
         s = next((v for k, v in sorted(summ.items())
@@ -288,9 +291,11 @@ def env_only(args, cfg, ctx, rank, world, rdzv):
     value = n * world * args.steps / dt
     bytes_launch = n * venv_bytes_per_env_step()
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, traffic_src, _ = pmc_traffic("venv_step_kernel<%d, %d>" % (B, D),
-                                          any_shape=True,
-                                          lib_sha=library_sha256())
+    # a summary of this library's env-only run at this env count and shape
+    # (tools/gpu_profile_env.sh records them in its _meta)
+    traffic, traffic_src, pmc = pmc_traffic(
+        "venv_step_kernel", any_shape=True, lib_sha=library_sha256(),
+        meta_match={"workload": "env_only", "envs": n, "bins": B, "dims": D})
     # the first-fit agent: 4 episodes of every env on the device evaluator
     # (its own kernel, whole episodes with the env state in registers)
     ff = heuristic_evaluate(ctx, "firstfit", B, D, n, 4, 20241008 + rank)
@@ -315,6 +320,9 @@ def env_only(args, cfg, ctx, rank, world, rdzv):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_over_algorithmic": (round(traffic / bytes_launch, 3)
+                                                  if traffic else None),
+                     "occupancy": pmc and pmc.get("occupancy"),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": venv_bytes_per_env_step(),
                      "avg_launch_ms": round(avg_ms, 5)},

@@ -144,7 +144,8 @@ constexpr int F_DB3 = F_B3 + 4;    // [32] matrix wave 0's db3 sums, per lane
 constexpr int F_SIMD = F_DB3 + 32; // [8] the SIMD each wave runs on (ints)
 #if XH_SP8_KL_TU
 constexpr int F_Q = F_SIMD + 8;    // [4 slots][64 bins] old distribution q
-constexpr int F_END = F_Q + 256;
+constexpr int F_KL = F_Q + 256;    // [4 matrix waves][32 lanes] KL sums (doubles)
+constexpr int F_END = F_KL + 256;
 #else
 constexpr int F_END = F_SIMD + 8;
 #endif
@@ -563,7 +564,11 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
 #endif
     } sm;
 #if XH_SP8_KL_TU
-    double kl_acc = 0.0;  // KL(q || p) of the valid rows this wave summed
+    // KL(q || p) of the valid rows this wave summed: per-lane doubles in LDS
+    // (ds_add_f64, nothing returned; a register pair held across the loop
+    // spilled)
+    double *kl_lane = reinterpret_cast<double *>(lf + F_KL) + 32 * s;
+    if (h == 0) kl_lane[l31] = 0.0;
 #endif
     auto softmax_stage = [&](int gi, int gpar, bool acc, int stage) {
       const int rs = gi & 3;
@@ -573,10 +578,6 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           sm.b3 = lf[F_B3];
           sm.z0 = lds4v(lf + F_Z + 4 * l31);
           sm.z1 = lds4v(lf + F_Z + 4 * (32 + l31));
-#if XH_SP8_KL_TU
-          sm.q0 = lf[F_Q + 64 * rs + l31];
-          sm.q1 = lf[F_Q + 64 * rs + 32 + l31];
-#endif
           if (s == 0) {
             // (wave 0's per-lane addresses recomputed here: held across the
             // loop they spilled)
@@ -597,6 +598,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           sm.se = half_sum32(sm.ex0 + sm.ex1);
           break;
         case 3: {
+#if XH_SP8_KL_TU
+          sm.q0 = lf[F_Q + 64 * rs + l31];  // (used a slot later)
+          sm.q1 = lf[F_Q + 64 * rs + 32 + l31];
+#endif
           const float se = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm.se), 31));
           const float rse = __builtin_amdgcn_rcpf(se);
           sm.p0 = sm.ex0 * rse;
@@ -619,8 +624,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           sm.gc = g1;
           const bool vld = __float_as_int(sm.po) != 0;
           if (vld && (gi & 3) == s && h == 0)
-            kl_acc += (double)(sm.q0 * logf(sm.q0 / sm.p0)) +
-                      (double)(sm.q1 * logf(sm.q1 / sm.p1));
+            __hip_atomic_fetch_add(kl_lane + opaque(l31),
+                                   (double)(sm.q0 * logf(sm.q0 / sm.p0)) +
+                                       (double)(sm.q1 * logf(sm.q1 / sm.p1)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           break;
         }
         case 5:
@@ -814,9 +821,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       // the workgroup's KL sum: the matrix waves' doubles in a fixed order
       // (the loop's last barrier is behind: F_Z is free; the vector waves
       // meet this barrier after their loop)
-      double v = kl_acc;
+      double v = h == 0 ? kl_lane[l31] : 0.0;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, kWave);
       double *kd = reinterpret_cast<double *>(lf + F_Z);
       if (l == 0) kd[s] = v;
       __syncthreads();

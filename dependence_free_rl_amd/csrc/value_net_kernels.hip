@@ -672,12 +672,14 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
     return !(e && e[0] == '0');
   }();
   const bool fuse = fuse_ok && a.env.B <= 64;
-  if (!fuse)
-    hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
-                       a.env.B, a.env.D, isum);
-  hipLaunchKernelGGL(w0_frag_kernel, dim3((2 * nkb * 64 + 255) / 256), dim3(256), 0, s,
-                     a.params, fuse ? nullptr : (const float *)isum, in, a.env.B, a.env.D, nkb,
-                     frag);
+  if (!a.w0frag_ready) {
+    if (!fuse)
+      hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
+                         a.env.B, a.env.D, isum);
+    hipLaunchKernelGGL(w0_frag_kernel, dim3((2 * nkb * 64 + 255) / 256), dim3(256), 0, s,
+                       a.params, fuse ? nullptr : (const float *)isum, in, a.env.B, a.env.D,
+                       nkb, frag);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int o1 = layer_off(a.w, 1), o2 = layer_off(a.w, 2);

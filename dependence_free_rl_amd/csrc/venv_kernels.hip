@@ -44,11 +44,40 @@ __device__ __forceinline__ void venv_obs_row(const int8_t *bp, const int8_t *ip,
   }
 }
 
+// One lane's D bytes of one bin row, as one load / store where D allows it
+// (D = 2: a 2-byte word; the row of an env starts at env * B * D, so bin * D
+// is 2-byte aligned), else byte by byte.
+template <int D>
+__device__ __forceinline__ void bin_load(const int8_t *p, int (&v)[D]) {
+  if constexpr (D == 2) {
+    const unsigned short w = *reinterpret_cast<const unsigned short *>(p);
+    v[0] = (int)(signed char)(w & 0xff);
+    v[1] = (int)(signed char)(w >> 8);
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = p[d];
+  }
+}
+template <int D>
+__device__ __forceinline__ void bin_store(int8_t *p, const int (&v)[D]) {
+  if constexpr (D == 2) {
+    *reinterpret_cast<unsigned short *>(p) =
+        (unsigned short)((v[0] & 0xff) | ((v[1] & 0xff) << 8));
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) p[d] = (int8_t)v[d];
+  }
+}
+
 // mode 0: environment::apply for every (masked) env -- bins[a] -= item; a new
 // item (2 draws) unless that bin went negative; done[e] = game_over after it.
 // mode 1: agent::step minus react -- skip the policy's draws, apply, reward =
 // game_over ? 0 : 1, reset (2 draws) on game over, then the env's stream
 // jumps over the other envs' draws of this step (reference order).
+// Every global load is issued first and unconditionally (an out-of-range
+// lane reads env 0's words; a masked or refused env's values are not used),
+// so their latencies overlap: one HBM round trip before the arithmetic
+// instead of three dependent ones (action -> item / bins -> stream state).
 template <int B, int D>
 __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   using S = VShape<B, D>;
@@ -58,18 +87,27 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   const int env = wave * S::EPW + el;
   const int seg0 = el * S::LPE;
   const bool in_range = env < a.N;
-  const bool on = in_range && (!a.mask || a.mask[env]);
-  int act = on ? a.action[env] : 0;
+  const size_t ec = in_range ? (size_t)env : 0;
+  int8_t *bp = a.bins + ec * S::BD;
+  int8_t *ip = a.items + ec * 4;
+  const int act_raw = a.action[ec];
+  const bool masked_in = !a.mask || a.mask[ec];
+  const unsigned itw = *reinterpret_cast<const unsigned *>(ip);
+  uint32_t x = a.rng[ec];
+  int v[S::BPL][D];
+#pragma unroll
+  for (int k = 0; k < S::BPL; ++k) bin_load<D>(bp + (k * 64 + li) * D, v[k]);
+
+  const bool on = in_range && masked_in;
+  int act = on ? act_raw : 0;
   if (on && (act < 0 || act >= B)) {  // refuse the env, flag the call
     if (li == 0) atomicOr(a.err, 1);
     act = -1;
   }
   const bool live = on && act >= 0;
-  int8_t *bp = a.bins + (size_t)(in_range ? env : 0) * S::BD;
-  int8_t *ip = a.items + (size_t)(in_range ? env : 0) * 4;
   int item[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) item[d] = live ? ip[d] : 0;
+  for (int d = 0; d < D; ++d) item[d] = live ? (int)(signed char)((itw >> (8 * d)) & 0xff) : 0;
   int nb[S::BPL][D];
   int neg_any = 0, neg_chosen = 0;
 #pragma unroll
@@ -77,8 +115,8 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
     const int bin = k * 64 + li;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const int v = live ? bp[bin * D + d] : 0;
-      nb[k][d] = bin == act ? v - item[d] : v;
+      const int vv = live ? v[k][d] : 0;
+      nb[k][d] = bin == act ? vv - item[d] : vv;
       neg_any |= nb[k][d] < 0;
       if (bin == act) neg_chosen |= nb[k][d] < 0;
     }
@@ -94,15 +132,14 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
     if (in_range && li == 0 && a.done) a.done[env] = 0;
     return;
   }
-  uint32_t x = a.rng[env];
   if (a.mode == 1) x = mstd_mulmod(x, a.skip_mul);  // the policy's draws
   const bool reset = a.mode == 1 && over;
 #pragma unroll
   for (int k = 0; k < S::BPL; ++k) {
-    const int bin = k * 64 + li;
+    int w[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d)
-      bp[bin * D + d] = (int8_t)(reset ? kCapacity : nb[k][d]);
+    for (int d = 0; d < D; ++d) w[d] = reset ? kCapacity : nb[k][d];
+    bin_store<D>(bp + (k * 64 + li) * D, w);
   }
   // every lane of the env draws the same item (redundant, register-only: no
   // cross-lane hand-off of the new item); the bin-0 lane writes the record
@@ -113,8 +150,10 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   if (reset) venv_item(a.env, x, nit);         // reset's get_item
   if (a.mode == 1) x = mstd_mulmod(x, a.jump_mul);
   if (li == 0) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) ip[d] = nit[d];
+    *reinterpret_cast<unsigned *>(ip) = (unsigned)(uint8_t)nit[0] |
+                                        ((unsigned)(uint8_t)nit[1] << 8) |
+                                        ((unsigned)(uint8_t)nit[2] << 16) |
+                                        ((unsigned)(uint8_t)nit[3] << 24);
     if (a.mode == 1 && a.reward) a.reward[env] = over ? 0.0f : 1.0f;
     if (a.done) a.done[env] = (uint8_t)over;
     a.rng[env] = x;

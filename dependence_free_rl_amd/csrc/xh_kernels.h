@@ -209,6 +209,10 @@ struct MlpArgs {
   // the forward stores for the backward (0: all, -1: none)
   void *w0frag;
   int act_rows;
+  // 1: w0frag already holds the fragments of these parameters (the trainer
+  // knows they did not change since the last forward prepared them): the
+  // forward skips its preparation launch
+  int w0frag_ready;
 };
 hipError_t mlp_forward(const MlpArgs &a, hipStream_t s);
 // Weight gradients of every layer into slab[split] (flat layout), data
@@ -398,6 +402,10 @@ hipError_t launch_policy_train_split8wh_kl(const PolicyTrainArgs &a, int grid,
 hipError_t launch_policy_train_spec8(const PolicyTrainArgs &a, int grid, hipStream_t s);
 // its KL-PPO build (policy_spec8_kl_kernels.o)
 hipError_t launch_policy_train_spec8_kl(const PolicyTrainArgs &a, int grid, hipStream_t s);
+// the wave-specialised config-2 epoch (policy_spec4_kernels.hip; one 8-wave
+// workgroup per CU: train_spec4_default says when the grid is one per CU)
+hipError_t launch_policy_train_spec4(const PolicyTrainArgs &a, int grid, hipStream_t s);
+bool train_spec4_default(int B, int D, int H1, int H2, int kl);
 hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
                                        hipStream_t s);
 hipError_t launch_policy_train_split4h(const PolicyTrainArgs &a, int grid,

@@ -81,6 +81,10 @@ struct xh_trainer {
   float *pslab = nullptr, *vslab = nullptr;
   float *vw0red = nullptr;  // value layer 0 on the reduced observation
   uint8_t *vw0frag = nullptr;  // W0's bf16 fragments (value_net_kernels.hip)
+  // vw0frag holds the fragments of the current value parameters (set by a
+  // bf16 value forward, cleared by every write of vp): the next iteration's
+  // first forward then skips the preparation launch
+  bool vfrag_ready = false;
   int pslab_stride = 0, vslab_stride = 0, pslab_n = 0, vslab_n = 0;
   float *pgrads = nullptr, *vgrad = nullptr;
   float *logits = nullptr, *probs = nullptr;
@@ -705,7 +709,10 @@ int do_learn(xh_trainer *t) {
   vm.term_list = t->end_list;
   vm.v_term = t->v_term;
   vm.term_n = t->n_end;
+  const bool vnet = std::strcmp(xh::value_kernel_name(vm), "vnet_bf16") == 0;
+  vm.w0frag_ready = vnet && t->vfrag_ready;
   CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
+  t->vfrag_ready = vnet;
   vm.rows = nullptr;
   vm.term_list = nullptr;
   vm.v_term = nullptr;
@@ -720,6 +727,7 @@ int do_learn(xh_trainer *t) {
       xh::value_reduced_slab(vm) ? xh::SlabAlias{t->cfg.value_h1, t->vl.Fin, t->cfg.bins,
                                t->cfg.dims}
                : xh::SlabAlias{0, 0, 0, 0};
+  t->vfrag_ready = false;  // the step below writes vp
   CHK(reduce_and_step(t, XH_VALUE, t->vslab, t->vslab_n, t->vslab_stride,
                       t->nv, t->vgrad, t->vp, al));
   // calculate_advantage (policy_gradient.h:220-281) on post-update values;
@@ -727,7 +735,9 @@ int do_learn(xh_trainer *t) {
   vm.max_rows = NS;
   vm.act[2] = t->v_state;
   vm.act_rows = -1;  // no backward reads these
+  vm.w0frag_ready = 0;  // (new parameters)
   CHK(timed(t, "value", [&]() { return xh::mlp_forward(vm, s); }));
+  t->vfrag_ready = vnet;
   va.v_state = t->v_state;
   va.row_g = nullptr;
   CHK(timed(t, "value", [&]() {
@@ -1604,6 +1614,7 @@ int xh_trainer_set_params(xh_trainer *t, int which, const float *host,
       return fail(XH_ERR_INVALID, "params: got %zu floats, model has %zu", n,
                   want);
     HIPCHK(hipSetDevice(t->ctx->device));
+    if (which != XH_POLICY) t->vfrag_ready = false;
     float *dst = which == XH_POLICY ? t->pp : t->vp;
     HIPCHK(copy_to_device(dst, host, n * 4, t->ctx->stream));
     HIPCHK(hipStreamSynchronize(t->ctx->stream));

@@ -95,15 +95,28 @@ def main(tag, trace, fetch, write, *sq_dirs):
             e["clock_ghz"] = g / 8.0 / ns
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in sq:
             e["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 1024)
+        # mean resident waves per SIMD (SQ_WAVE_CYCLES counts quad-cycles,
+        # MI355X_MICROARCH.md) and where the waves' cycles went
+        wc = sq.get("SQ_WAVE_CYCLES")
+        if g and wc:
+            e["occupancy"] = 4.0 * wc / (g / 8.0 * 1024)
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in sq:
+                    e[c.lower() + "_frac"] = sq[c] / wc
     summary["_meta"] = {
         "tag": tag,
         "library_sha256": library_sha256(here),
         "created": datetime.datetime.now(datetime.timezone.utc).isoformat(
             timespec="seconds")}
+    # PMC_META (JSON object): what the profiled run was, for lookups that
+    # depend on more than the kernel's name (bench.py --env-only matches the
+    # env count: its bytes per launch scale with it)
+    if os.environ.get("PMC_META"):
+        summary["_meta"].update(json.loads(os.environ["PMC_META"]))
     with open(os.path.join(out, "%s_pmc_summary.json" % tag), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    print(json.dumps({k: v for k, v in summary.items() if "policy_train" in k},
-                     indent=1))
+    key = os.environ.get("PMC_PRINT", "policy_train")
+    print(json.dumps({k: v for k, v in summary.items() if key in k}, indent=1))
 
 
 if __name__ == "__main__":
