@@ -2501,7 +2501,7 @@ int rollout_grid(int B, int D, int H1, int H2) {
   return 2 * cu_count();
 }
 int policy_train_grid(int B, int D, int H1, int H2, int kl) {
-  // the wave-specialised config-2 kernel: one 8-wave workgroup per CU
+  // the wave-specialised config-2 kernel (opt-in): one 8-wave workgroup per CU
   if (train_spec4_default(B, D, H1, H2, kl)) return cu_count();
 #define X(XB, XD, XH1, XH2)                                     \
   if (B == XB && D == XD && H1 == XH1 && H2 == XH2) {          \

@@ -46,6 +46,28 @@
 #define XH_SP4_VFIRST 1
 #endif
 
+// Phase stamps (trace build, tools/build_trace_sp4.sh: -DXH_DIAG_TRACE=1,
+// run with XH_PHASE_TRACE=1): lane 0 of every wave of the first kTraceBlocks
+// workgroups records the cycle counter at 0 A(j) start, 1 its phase-A work
+// done, 2 after the A barrier, 3 its phase-B work done, 4 after the B barrier
+// (5 .. 7 = 4) for groups j < kTraceGroups - 1
+#ifndef XH_DIAG_TRACE
+#define XH_DIAG_TRACE 0
+#endif
+#if XH_DIAG_TRACE
+#define SP4_STAMP(a, gi, w, lane, slot)                                               \
+  do {                                                                                \
+    if ((a).trace && blockIdx.x < kTraceBlocks && (gi) < kTraceGroups - 1 && (lane) == 0) \
+      for (int k_ = (slot); k_ < ((slot) == 4 ? kTraceSlots : (slot) + 1); ++k_)      \
+        (a).trace[((blockIdx.x * kTraceGroups + (gi)) * 8 + (w)) * kTraceSlots + k_] = \
+            clock64();                                                                \
+  } while (0)
+#else
+#define SP4_STAMP(a, gi, w, lane, slot) \
+  do {                                  \
+  } while (0)
+#endif
+
 namespace xh {
 namespace sp4 {
 
@@ -271,9 +293,20 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
     for (int q = 0; q < 4; ++q)
       mwb[q] = opaque(wr_base(32 * rt + l31, q, h, kNY) + 1024 * ot + L_MK);
 
-    f32x16s accW2;
+    // layer 2's bias (its accumulator's start) and w3 / S2 of this lane's
+    // 16 outputs o = 32 ot + 8 q + 4 h + u, held for the launch
+    float b2r[16], w3r[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) accW2[e] = 0.0f;
+    for (int e = 0; e < 16; ++e) {
+      const int o = 32 * ot + 8 * (e >> 2) + 4 * h + (e & 3);
+      b2r[e] = P[PL.ob2() + o] * S2;
+      w3r[e] = P[PL.ow3() + o] * (1.0f / S2);
+    }
+    // dW2 in two accumulators (K-steps 0-1 and 2-3 of every group, summed at
+    // the write-out: no dependent MFMA chain)
+    f32x16s accW2, accW2b;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accW2[e] = accW2b[e] = 0.0f;
     float acc3[16], accb2[16], accb3 = 0.0f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc3[e] = accb2[e] = 0.0f;
@@ -314,48 +347,68 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
     // layer 2 of the group in the H1 image: C[o][r] = S2 (b2 + W2 . H1) for
     // this wave's 32 o (registers) x env rt (lanes), 4 K-steps of three f16
     // MFMAs; the B operand one step ahead (ping-pong); task(k) after MFMA k
+    // (two accumulators, K-steps 0-1 and 2-3, their MFMAs interleaved: a
+    // dependent 32x32x16 MFMA waits for its predecessor's whole result, so
+    // one chain of 12 would expose every MFMA's latency; summed at the end)
     auto layer2 = [&](f32x16s &c, auto &&task) {
+      f32x16s c1;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 b2 = lds4v(lf + F_B2 + 32 * ot + 8 * q + 4 * h);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) c[4 * q + u] = b2[u];
+      for (int e = 0; e < 16; ++e) {
+        c[e] = b2r[e];
+        c1[e] = 0.0f;
       }
-      f16x8 bh[2], bl[2];
+      f16x8 bh[4], bl[4];
       auto ldB = [&](int ks) {
         const int o = ((ks & 1) ? rbH1 : rbH0) + 1024 * (ks >> 1);
-        bh[ks & 1] = ld8h(o);
-        bl[ks & 1] = ld8h(o + kImg);
+        bh[ks] = ld8h(o);
+        bl[ks] = ld8h(o + kImg);
       };
       ldB(0);
+      ldB(2);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int cb = ks & 1;
-        if (ks + 1 < 4) ldB(ks + 1);
+      for (int kp = 0; kp < 2; ++kp) {  // K-steps kp (-> c) and 2 + kp (-> c1)
+        const int ka = kp, kb = 2 + kp;
+        if (kp == 0) {
+          ldB(1);
+          ldB(3);
+        }
         FENCE();
-        c = mfma_f16(wl[ks][1], bh[cb], c);  // the three products,
+        c = mfma_f16(wl[ka][1], bh[ka], c);  // the three products,
         FENCE();                              // small terms first
-        task(3 * ks);
+        task(6 * kp);
         FENCE();
-        c = mfma_f16(wl[ks][0], bl[cb], c);
+        c1 = mfma_f16(wl[kb][1], bh[kb], c1);
         FENCE();
-        task(3 * ks + 1);
+        task(6 * kp + 1);
         FENCE();
-        c = mfma_f16(wl[ks][0], bh[cb], c);
+        c = mfma_f16(wl[ka][0], bl[ka], c);
         FENCE();
-        task(3 * ks + 2);
+        task(6 * kp + 2);
+        FENCE();
+        c1 = mfma_f16(wl[kb][0], bl[kb], c1);
+        FENCE();
+        task(6 * kp + 3);
+        FENCE();
+        c = mfma_f16(wl[ka][0], bh[ka], c);
+        FENCE();
+        task(6 * kp + 4);
+        FENCE();
+        c1 = mfma_f16(wl[kb][0], bh[kb], c1);
+        FENCE();
+        task(6 * kp + 5);
         FENCE();
       }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) c[e] += c1[e];
     };
     // partial logits of rows 32 rt + l31 over this wave's o -> F_Z
     auto partials = [&](const f32x16s &c) {
       float zq[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x4 w3 = lds4v(lf + F_W3 + 32 * ot + 8 * q + 4 * h);
-        float z = relu(c[4 * q]) * w3[0];
+        float z = relu(c[4 * q]) * w3r[4 * q];
 #pragma unroll
-        for (int u = 1; u < 4; ++u) z = fmaf(relu(c[4 * q + u]), w3[u], z);
+        for (int u = 1; u < 4; ++u) z = fmaf(relu(c[4 * q + u]), w3r[4 * q + u], z);
         zq[q] = z;
       }
       const float z = add_halves((zq[0] + zq[1]) + (zq[2] + zq[3]));
@@ -453,38 +506,54 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
     // B (the three parts) one step ahead; task(k) after MFMA k
     auto dw2 = [&](int ms, auto &&task) {
       const int mb = kImg * ms;  // (trM holds L_MK)
-      bf16x8 A[2], Bv[2][3];
+      bf16x8 A[4], Bv[4][3];
       auto ldB = [&](int ks) {
         const int ob = 1024 * (ks >> 1) + ((ks & 1) ? rbg1 : rbg0);
-        Bv[ks & 1][0] = ld8(ob);
-        Bv[ks & 1][1] = ld8(ob + kImg);
-        Bv[ks & 1][2] = ld8(ob + 2 * kImg);
+        Bv[ks][0] = ld8(ob);
+        Bv[ks][1] = ld8(ob + kImg);
+        Bv[ks][2] = ld8(ob + 2 * kImg);
       };
       auto ldA = [&](int ks) {
         const int o = mb + 1024 * (kNY * ks + ot);
-        A[ks & 1] = ldtr(trM0 + o, trM1 + o);
+        A[ks] = ldtr(trM0 + o, trM1 + o);
       };
       ldB(0);
       ldA(0);
+      ldB(2);
+      ldA(2);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int cb = ks & 1;
-        if (ks + 1 < 4) {
-          ldA(ks + 1);
-          ldB(ks + 1);
+      for (int kp = 0; kp < 2; ++kp) {  // K-steps kp (-> accW2), 2 + kp (-> accW2b)
+        const int ca = kp, cb = 2 + kp;
+        if (kp == 0) {
+          ldA(1);
+          ldB(1);
+          ldA(3);
+          ldB(3);
         }
         FENCE();
-        accW2 = mfma_bf16(A[cb], Bv[cb][2], accW2);
+        accW2 = mfma_bf16(A[ca], Bv[ca][2], accW2);
         FENCE();
-        task(3 * ks);
+        task(6 * kp);
         FENCE();
-        accW2 = mfma_bf16(A[cb], Bv[cb][1], accW2);
+        accW2b = mfma_bf16(A[cb], Bv[cb][2], accW2b);
         FENCE();
-        task(3 * ks + 1);
+        task(6 * kp + 1);
         FENCE();
-        accW2 = mfma_bf16(A[cb], Bv[cb][0], accW2);
+        accW2 = mfma_bf16(A[ca], Bv[ca][1], accW2);
         FENCE();
-        task(3 * ks + 2);
+        task(6 * kp + 2);
+        FENCE();
+        accW2b = mfma_bf16(A[cb], Bv[cb][1], accW2b);
+        FENCE();
+        task(6 * kp + 3);
+        FENCE();
+        accW2 = mfma_bf16(A[ca], Bv[ca][0], accW2);
+        FENCE();
+        task(6 * kp + 4);
+        FENCE();
+        accW2b = mfma_bf16(A[cb], Bv[cb][0], accW2b);
+        FENCE();
+        task(6 * kp + 5);
         FENCE();
       }
     };
@@ -506,10 +575,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
 
     // ---- pipeline prologue (barriers as the vector path's)
     f32x16s c;
+    // the staging loads run two periods ahead of their stores (a period is
+    // short here: one phase would expose the HBM latency at every store):
+    // group g's raw words in rr[g & 1]
+    Raw rr[2];
     if (s == 0) {
       stage_store(stage_load(0), 0);
       stage_store(stage_load(1), 1);
       stage_store(stage_load(2), 2);
+      rr[1] = stage_load(3);
     }
     __syncthreads();  // P1: rows staged          (vector: L1(0))
     __syncthreads();  // P2
@@ -521,18 +595,22 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
     __syncthreads();  // P4
     auto period = [&](int j, auto P) {
       constexpr int par = decltype(P)::value;
-      Raw raw;
-      if (s == 0) raw = stage_load(j + 3);
+      SP4_STAMP(a, j, w, l, 0);
+      if (s == 0) rr[par] = stage_load(j + 4);  // (group j + 4: rr[(j + 4) & 1])
       // A(j): layer 2 of group j+1, its partial logits after
       layer2(c, no_task);
       partials(c);
+      SP4_STAMP(a, j, w, l, 1);
       __syncthreads();
+      SP4_STAMP(a, j, w, l, 2);
       // B(j): dW2 of group j with group j+1's softmax, masks and dW3 / db2
-      // sums in its MFMA slots
-      if (s == 0) stage_store(raw, (j + 3) & 3);
+      // sums in its MFMA slots; group j+3's rows (loaded a period ago) staged
+      if (s == 0) stage_store(rr[par ^ 1], (j + 3) & 3);
       const bool acc = j + 1 < J;
       dw2(par, [&](int k) { b_task(c, j + 1, 1 - par, acc, k); });
+      SP4_STAMP(a, j, w, l, 3);
       __syncthreads();
+      SP4_STAMP(a, j, w, l, 4);
     };
     for (int j = 0; j < J; j += 2) {
       period(j, Par<0>{});
@@ -544,7 +622,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int o = 32 * ot + 8 * (e >> 2) + 4 * h + (e & 3);
-      slab[PL.oW2() + o * kH + 32 * it2 + l31] = (accW2[e] * rSH) * w3g[o];
+      slab[PL.oW2() + o * kH + 32 * it2 + l31] = ((accW2[e] + accW2b[e]) * rSH) * w3g[o];
     }
     // dW3 / db2 of o = 32 ot + 8 (e >> 2) + 4 h + (e & 3): sums over the 32
     // lanes (rows) of the half, env B's waves hand theirs to env A's
@@ -693,21 +771,22 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
       const float *gv = lf + F_G + 128 * gpar + 32 * rt;
       const float *xv = lf + F_X + (gi & 3) * 64 + 32 * rt;
       const float b1 = ia_of(gi) ? b1a : b1b;
-      f16x8 A[2];
+      f16x8 A[4];
       auto ldA = [&](int ks) {
-        A[ks & 1] = ld8h(((ks & 1) ? rbm1 : rbm0) + mb + 1024 * (ks >> 1));
+        A[ks] = ld8h(((ks & 1) ? rbm1 : rbm0) + mb + 1024 * (ks >> 1));
       };
-      f32x4 ring[2][2];  // [block & 1][x, g]
+      f32x4 ring[3][2];  // [block % 3][x, g]: two blocks ahead
       auto ld2 = [&](int q) {
-        ring[q & 1][0] = lds4v(xv + 8 * q + 4 * h);
-        ring[q & 1][1] = lds4v(gv + 8 * q + 4 * h);
+        ring[q % 3][0] = lds4v(xv + 8 * q + 4 * h);
+        ring[q % 3][1] = lds4v(gv + 8 * q + 4 * h);
       };
       ld2(0);
+      ld2(1);
       float xx[4];
       unsigned ph[2], pm[2], pl[2];
       auto gh_task = [&](int k) {  // k = 0 .. 15: block q = k / 4
         const int q = k >> 2;
-        const f32x4(&o)[2] = ring[q & 1];
+        const f32x4(&o)[2] = ring[q % 3];
         switch (k & 3) {
           case 0:
 #pragma unroll
@@ -716,7 +795,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
               hk[4 * q + u] = hv;
               xx[u] = hv * o[1][u];
             }
-            if (q + 1 < 4) ld2(q + 1);
+            if (q + 2 < 4) ld2(q + 2);
             break;
           case 1:
             split3_pair(xx[0], xx[1], ph[0], pm[0], pl[0]);
@@ -731,41 +810,66 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
           }
         }
       };
+      // (two accumulators, K-steps 0-1 and 2-3, interleaved; summed after)
+      f32x16s dh1;
       ldA(0);
+      ldA(2);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int ca = ks & 1;
-        if (ks + 1 < 4) ldA(ks + 1);
+      for (int kp = 0; kp < 2; ++kp) {
+        const int ka = kp, kb = 2 + kp;
+        if (kp == 0) {
+          ldA(1);
+          ldA(3);
+        }
         FENCE();
-        if (ks == 0)
-          dh = mfma_f16(A[ca], wd[ks][1], f32x16s{});
+        if (kp == 0)
+          dh = mfma_f16(A[ka], wd[ka][1], f32x16s{});
         else
-          dh = mfma_f16(A[ca], wd[ks][1], dh);
+          dh = mfma_f16(A[ka], wd[ka][1], dh);
         FENCE();
-        gh_task(4 * ks);
-        gh_task(4 * ks + 1);
+        gh_task(8 * kp);
+        gh_task(8 * kp + 1);
         FENCE();
-        dh = mfma_f16(A[ca], wd[ks][0], dh);
+        if (kp == 0)
+          dh1 = mfma_f16(A[kb], wd[kb][1], f32x16s{});
+        else
+          dh1 = mfma_f16(A[kb], wd[kb][1], dh1);
         FENCE();
-        gh_task(4 * ks + 2);
-        gh_task(4 * ks + 3);
+        gh_task(8 * kp + 2);
+        gh_task(8 * kp + 3);
+        FENCE();
+        dh = mfma_f16(A[ka], wd[ka][0], dh);
+        FENCE();
+        gh_task(8 * kp + 4);
+        gh_task(8 * kp + 5);
+        FENCE();
+        dh1 = mfma_f16(A[kb], wd[kb][0], dh1);
+        FENCE();
+        gh_task(8 * kp + 6);
+        gh_task(8 * kp + 7);
         FENCE();
       }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dh[e] += dh1[e];
     };
     // B(gi): dW1 / db1 / item sums of group gi: d = relu'(H1) dH1; sums
     // d g x, d g (g, g x staged by the matrix waves), two partial sums each
     auto dw1 = [&](int gi, int gpar, const f32x16s &hk, const f32x16s &dh) {
       const float *gv = lf + F_G + 128 * gpar + 32 * rt;
       float a0[2] = {0.0f, 0.0f}, ag[2] = {0.0f, 0.0f};
+      f32x4 g4[4], gx4[4];  // every load issued before the first use
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x4 g4 = lds4v(gv + 8 * q + 4 * h);
-        const f32x4 gx4 = lds4v(gv + 64 + 8 * q + 4 * h);
+        g4[q] = lds4v(gv + 8 * q + 4 * h);
+        gx4[q] = lds4v(gv + 64 + 8 * q + 4 * h);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float m = hk[4 * q + u] > 0.0f ? dh[4 * q + u] : 0.0f;
-          a0[u & 1] = fmaf(m, gx4[u], a0[u & 1]);
-          ag[u & 1] = fmaf(m, g4[u], ag[u & 1]);
+          a0[u & 1] = fmaf(m, gx4[q][u], a0[u & 1]);
+          ag[u & 1] = fmaf(m, g4[q][u], ag[u & 1]);
         }
       }
       w0 += a0[0] + a0[1];
@@ -785,11 +889,16 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec4_kernel(PolicyT
     __syncthreads();  // P4                       (matrix: SM(0))
     auto period = [&](int j, auto P) {
       constexpr int par = decltype(P)::value;
+      SP4_STAMP(a, j, w, l, 0);
       dh_gh(j, par, hk, dh);
+      SP4_STAMP(a, j, w, l, 1);
       __syncthreads();  // A(j)
+      SP4_STAMP(a, j, w, l, 2);
       dw1(j, par, hk, dh);
       layer1(j + 2);
+      SP4_STAMP(a, j, w, l, 3);
       __syncthreads();  // B(j)
+      SP4_STAMP(a, j, w, l, 4);
     };
     for (int j = 0; j < J; j += 2) {
       period(j, Par<0>{});

@@ -8,10 +8,10 @@
 //                                  policy_train_split8wh_kernel)
 //   128 bins, 3-D, [128,128] (config 5)      policy_train_split8x_kernel
 //                                  (KL-PPO: policy_train_split8x_kl_kernel)
-//   32 bins, 1-D, [64,64] (config 2)         policy_train_spec4_kernel
+//   32 bins, 1-D, [64,64] (config 2)         policy_train_split4h_kernel
 //                                  (KL-PPO: policy_train_split4h_kl_kernel;
-//                                  XH_TRAIN_KERNEL=split4h: the earlier
-//                                  policy_train_split4h_kernel)
+//                                  XH_TRAIN_KERNEL=spec4: the wave-specialised
+//                                  policy_train_spec4_kernel)
 // and the f32-MFMA kernels of policy_kernels.hip for every other shape (KL-PPO
 // included), and under XH_TRAIN_KERNEL=f32 (the accuracy reference of the split
 // kernels' tests).
@@ -54,8 +54,16 @@ static bool train_kernel_is(const char *name) {
 }
 #endif
 
+// the wave-specialised config-2 kernel (policy_spec4_kernels.hip, round 6) is
+// opt-in: XH_TRAIN_KERNEL=spec4.  Parity-green, but 2-3% slower than
+// policy_train_split4h_kernel on paired boxes (0.068 against 0.0663 ms per
+// epoch: its matrix waves' phase B bounds the group)
+static bool spec4_selected() {
+  const char *ov = train_override();
+  return ov && std::strcmp(ov, "spec4") == 0;
+}
 bool train_spec4_default(int B, int D, int H1, int H2, int kl) {
-  return !kl && !train_override() && B == kSplit4hBins && D == 1 && H1 == 64 && H2 == 64;
+  return !kl && spec4_selected() && B == kSplit4hBins && D == 1 && H1 == 64 && H2 == 64;
 }
 
 bool policy_train_split_supported(const PolicyTrainArgs &a, int H1, int H2) {
@@ -81,9 +89,9 @@ hipError_t launch_policy_train_split(const PolicyTrainArgs &a, int grid,
   info->math = kMathSplitTrainF16;
   const char *ov = train_override();
   if (a.env.B == kSplit4hBins) {
-    // the wave-specialised kernel for PPO / actor-critic; the KL-PPO build
-    // and XH_TRAIN_KERNEL=split4h (A/B runs) run policy_train_split4h_kernel
-    if (!ov && a.algo != kKLPPO) {
+    // policy_train_split4h_kernel (and its KL-PPO build); the
+    // wave-specialised form under XH_TRAIN_KERNEL=spec4 (A/B runs)
+    if (spec4_selected() && a.algo != kKLPPO) {
       info->name = "policy_train_spec4_kernel";
       return launch_policy_train_spec4(a, grid, s);
     }

@@ -78,11 +78,21 @@ __device__ __forceinline__ void bin_store(int8_t *p, const int (&v)[D]) {
 // lane reads env 0's words; a masked or refused env's values are not used),
 // so their latencies overlap: one HBM round trip before the arithmetic
 // instead of three dependent ones (action -> item / bins -> stream state).
+// XCD-aware block order: workgroups are dispatched round-robin over the 8
+// XCDs (XCD = block index mod 8), each with its own L2; block b takes the
+// env range of block (b mod 8) G / 8 + b / 8, so an XCD steps one contiguous
+// run of envs and the 4-byte per-env records sharing a 128-byte line
+// (action, item, stream state, reward) are fetched by one L2, not eight
+__device__ __forceinline__ int xcd_block() {
+  const int G = (int)gridDim.x, b = (int)blockIdx.x;
+  return (G & 7) == 0 ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
+
 template <int B, int D>
 __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   using S = VShape<B, D>;
   const int lane = threadIdx.x & 63;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int wave = (xcd_block() * (int)blockDim.x + (int)threadIdx.x) >> 6;
   const int el = lane / S::LPE, li = lane % S::LPE;
   const int env = wave * S::EPW + el;
   const int seg0 = el * S::LPE;

@@ -402,8 +402,9 @@ hipError_t launch_policy_train_split8wh_kl(const PolicyTrainArgs &a, int grid,
 hipError_t launch_policy_train_spec8(const PolicyTrainArgs &a, int grid, hipStream_t s);
 // its KL-PPO build (policy_spec8_kl_kernels.o)
 hipError_t launch_policy_train_spec8_kl(const PolicyTrainArgs &a, int grid, hipStream_t s);
-// the wave-specialised config-2 epoch (policy_spec4_kernels.hip; one 8-wave
-// workgroup per CU: train_spec4_default says when the grid is one per CU)
+// the wave-specialised config-2 epoch (policy_spec4_kernels.hip, opt-in by
+// XH_TRAIN_KERNEL=spec4; one 8-wave workgroup per CU: train_spec4_default
+// says when the grid is one per CU)
 hipError_t launch_policy_train_spec4(const PolicyTrainArgs &a, int grid, hipStream_t s);
 bool train_spec4_default(int B, int D, int H1, int H2, int kl);
 hipError_t launch_policy_train_split8wg(const PolicyTrainArgs &a, int grid,
