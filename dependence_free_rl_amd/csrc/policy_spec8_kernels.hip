@@ -106,6 +106,17 @@
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
 #endif
+// XH_SP8_DHI / XH_SP8_L2I (A/B builds): dH1's (vector) / layer 2's (matrix)
+// 16 steps in the order (t = st & 1, ks = st >> 1), alternating the two
+// r-tiles' accumulators, instead of all of r-tile 0's steps first (a
+// dependent MFMA waits for its predecessor's result; the per-accumulator
+// order of the products is unchanged: bit-identical)
+#ifndef XH_SP8_DHI
+#define XH_SP8_DHI 0
+#endif
+#ifndef XH_SP8_L2I
+#define XH_SP8_L2I 0
+#endif
 #ifndef XH_SP8_VBF
 #define XH_SP8_VBF 0
 #endif
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       }
       f16x8 bh[2], bl[2];
       auto ldB = [&](int st) {
-        const int t = st >> 3, ks = st & 7;
+        const int t = XH_SP8_L2I ? st & 1 : st >> 3, ks = XH_SP8_L2I ? st >> 1 : st & 7;
         const int o = ((ks & 1) ? rbH1 : rbH0) + 8192 * t + 1024 * (ks >> 1);
         bh[st & 1] = ld8h(o);
         bl[st & 1] = ld8h(o + kImg);
@@ -503,7 +514,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       ldB(0);
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
-        const int t = st >> 3, ks = st & 7, cb = st & 1;
+        const int t = XH_SP8_L2I ? st & 1 : st >> 3, ks = XH_SP8_L2I ? st >> 1 : st & 7,
+                  cb = st & 1;
         if (st + 1 < 16) ldB(st + 1);
         FENCE();
         c[t] = mfma_f16(wl[ks][1], bh[cb], c[t]);  // the three products,
@@ -795,6 +807,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       if (s == 0) raw = stage_load(j + 3);
       // A(j): layer 2 of group j+1; r-tile 0's partial logits in r-tile 1's
       // MFMA slots, r-tile 1's after
+#if XH_SP8_L2I
+      // (r-tile 0 is complete only after step 14: its partials after it,
+      // r-tile 1's at the tail)
+      if (SP8_RUN(1 | 32)) layer2(c, [&](int k) {
+        if (k == 40) ld_w3(0);
+        if (k == 41) ld_w3(1);
+      });
+      if (SP8_RUN(1)) {
+        partial_q(c[0], 0);
+        ld_w3(2);
+        partial_q(c[0], 1);
+        ld_w3(3);
+        partial_q(c[0], 2);
+        partial_q(c[0], 3);
+        partial_store(0);
+        partials_tail(c[1], 1);
+      }
+#else
       if (SP8_RUN(1 | 32)) layer2(c, [&](int k) {
         // r-tile 0's blocks q at slots 27 + 3q, their w3 three slots ahead
         if (k >= 24 && k < 36 && k % 3 == 0) ld_w3((k - 24) / 3);
@@ -802,6 +832,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
         if (k == 40) partial_store(0);
       });
       if (SP8_RUN(1)) partials_tail(c[1], 1);
+#endif
       __syncthreads();
       // B(j): dW2 of group j with group j+1's softmax, dW3 / db2 sums and
       // masks in its MFMA slots
@@ -1019,7 +1050,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       const float b1 = b1_of(gi);
       f16x8 A[2];
       auto ldA = [&](int st) {
-        const int t = st >> 3, ks = st & 7;
+        const int t = XH_SP8_DHI ? st & 1 : st >> 3, ks = XH_SP8_DHI ? st >> 1 : st & 7;
         A[st & 1] = ld8h(((ks & 1) ? rbm1 : rbm0) + mb + 8192 * t + 1024 * (ks >> 1));
       };
       f32x4 ring[3][3];  // [block % 3][x0, x1, g]
@@ -1066,7 +1097,8 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       ldA(0);
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
-        const int t = st >> 3, ks = st & 7, ca = st & 1;
+        const int t = XH_SP8_DHI ? st & 1 : st >> 3, ks = XH_SP8_DHI ? st >> 1 : st & 7,
+                  ca = st & 1;
         if (st + 1 < 16) ldA(st + 1);
         VAFENCE();
         if (ks == 0)

@@ -25,6 +25,22 @@ struct VShape {
   static constexpr int BD = B * D;
 };
 
+// The step kernel's layout: four consecutive bins per lane (their 4 D bytes
+// as D aligned 32-bit words), so 64 / (B / 4) envs share a wave.  The step
+// is issue-bound, not HBM-bound: every lane of an env draws the env's item
+// (two engine draws and a double-precision canonical, register-only) and
+// steps its stream with 64-bit modular multiplies, so the instruction count
+// per byte falls with the bins a lane carries (round 6: one env per wave at
+// 64 bins gave 1.27 TB/s at 1M envs with the traffic at its algorithmic
+// bytes, counters: 25% issuing, 40% issue stalls, 35% waiting on memory).
+template <int B, int D>
+struct VStepShape {
+  static constexpr int BPL = 4;            // bins per lane (contiguous)
+  static constexpr int LPE = B / BPL;      // lanes per env
+  static constexpr int EPW = 64 / LPE;     // envs per wave
+  static constexpr int BD = B * D;
+};
+
 // draw one item (get_item: bernoulli(0.4) over generate_canonical<double>)
 __device__ __forceinline__ void venv_item(const EnvDesc &E, uint32_t &x,
                                           int8_t *ip) {
@@ -41,31 +57,6 @@ __device__ __forceinline__ void venv_obs_row(const int8_t *bp, const int8_t *ip,
   for (int d = 0; d < D; ++d) {
     o[d] = (float)bp[d] / (float)kCapacity;
     o[D + d] = (float)ip[d] / (float)kCapacity;
-  }
-}
-
-// One lane's D bytes of one bin row, as one load / store where D allows it
-// (D = 2: a 2-byte word; the row of an env starts at env * B * D, so bin * D
-// is 2-byte aligned), else byte by byte.
-template <int D>
-__device__ __forceinline__ void bin_load(const int8_t *p, int (&v)[D]) {
-  if constexpr (D == 2) {
-    const unsigned short w = *reinterpret_cast<const unsigned short *>(p);
-    v[0] = (int)(signed char)(w & 0xff);
-    v[1] = (int)(signed char)(w >> 8);
-  } else {
-#pragma unroll
-    for (int d = 0; d < D; ++d) v[d] = p[d];
-  }
-}
-template <int D>
-__device__ __forceinline__ void bin_store(int8_t *p, const int (&v)[D]) {
-  if constexpr (D == 2) {
-    *reinterpret_cast<unsigned short *>(p) =
-        (unsigned short)((v[0] & 0xff) | ((v[1] & 0xff) << 8));
-  } else {
-#pragma unroll
-    for (int d = 0; d < D; ++d) p[d] = (int8_t)v[d];
   }
 }
 
@@ -90,7 +81,7 @@ __device__ __forceinline__ int xcd_block() {
 
 template <int B, int D>
 __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
-  using S = VShape<B, D>;
+  using S = VStepShape<B, D>;
   const int lane = threadIdx.x & 63;
   const int wave = (xcd_block() * (int)blockDim.x + (int)threadIdx.x) >> 6;
   const int el = lane / S::LPE, li = lane % S::LPE;
@@ -104,9 +95,19 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   const bool masked_in = !a.mask || a.mask[ec];
   const unsigned itw = *reinterpret_cast<const unsigned *>(ip);
   uint32_t x = a.rng[ec];
+  // this lane's bins li * 4 .. li * 4 + 3: D words, byte k * D + d = bin k, dim d
+  uint32_t wv[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q)
+    wv[q] = reinterpret_cast<const uint32_t *>(bp + li * S::BPL * D)[q];
   int v[S::BPL][D];
 #pragma unroll
-  for (int k = 0; k < S::BPL; ++k) bin_load<D>(bp + (k * 64 + li) * D, v[k]);
+  for (int k = 0; k < S::BPL; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int j = k * D + d;
+      v[k][d] = (int)(signed char)((wv[j >> 2] >> (8 * (j & 3))) & 0xff);
+    }
 
   const bool on = in_range && masked_in;
   int act = on ? act_raw : 0;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   int neg_any = 0, neg_chosen = 0;
 #pragma unroll
   for (int k = 0; k < S::BPL; ++k) {
-    const int bin = k * 64 + li;
+    const int bin = li * S::BPL + k;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int vv = live ? v[k][d] : 0;
@@ -144,12 +145,20 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   }
   if (a.mode == 1) x = mstd_mulmod(x, a.skip_mul);  // the policy's draws
   const bool reset = a.mode == 1 && over;
+  {
+    uint32_t ow[D];
 #pragma unroll
-  for (int k = 0; k < S::BPL; ++k) {
-    int w[D];
+    for (int q = 0; q < D; ++q) ow[q] = 0u;
 #pragma unroll
-    for (int d = 0; d < D; ++d) w[d] = reset ? kCapacity : nb[k][d];
-    bin_store<D>(bp + (k * 64 + li) * D, w);
+    for (int k = 0; k < S::BPL; ++k)
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int j = k * D + d;
+        ow[j >> 2] |= (uint32_t)((reset ? kCapacity : nb[k][d]) & 0xff) << (8 * (j & 3));
+      }
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+      reinterpret_cast<uint32_t *>(bp + li * S::BPL * D)[q] = ow[q];
   }
   // every lane of the env draws the same item (redundant, register-only: no
   // cross-lane hand-off of the new item); the bin-0 lane writes the record
@@ -171,7 +180,7 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   if (a.obs) {  // observation::to_vector of the resulting state
 #pragma unroll
     for (int k = 0; k < S::BPL; ++k) {
-      const int bin = k * 64 + li;
+      const int bin = li * S::BPL + k;
       float *o = a.obs + ((size_t)env * B + bin) * 2 * D;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
@@ -255,6 +264,12 @@ static dim3 venv_grid(int N, int B) {
   const long waves = (N + epw - 1) / epw;
   return dim3((unsigned)((waves + 3) / 4));
 }
+// the step kernel's (VStepShape: 4 bins per lane)
+static dim3 venv_step_grid(int N, int B) {
+  const int epw = 64 / (B / 4);
+  const long waves = (N + epw - 1) / epw;
+  return dim3((unsigned)((waves + 3) / 4));
+}
 
 hipError_t launch_venv(const VenvArgs &a, int op, hipStream_t s) {
   const int B = a.env.B, D = a.env.D;
@@ -262,7 +277,7 @@ hipError_t launch_venv(const VenvArgs &a, int op, hipStream_t s) {
 #define X(XB, XD)                                                            \
   if (B == XB && D == XD) {                                                  \
     if (op == kVenvStep)                                                     \
-      hipLaunchKernelGGL((venv_step_kernel<XB, XD>), venv_grid(a.N, B),      \
+      hipLaunchKernelGGL((venv_step_kernel<XB, XD>), venv_step_grid(a.N, B), \
                          dim3(256), 0, s, a);                                \
     else if (op == kVenvReset)                                               \
       hipLaunchKernelGGL((venv_reset_kernel<XB, XD>), venv_grid(a.N, B),     \
