@@ -25,17 +25,28 @@ struct VShape {
   static constexpr int BD = B * D;
 };
 
-// The step kernel's layout: four consecutive bins per lane (their 4 D bytes
-// as D aligned 32-bit words), so 64 / (B / 4) envs share a wave.  The step
-// is issue-bound, not HBM-bound: every lane of an env draws the env's item
+// The step kernel's layout: XH_VENV_BPL (16) consecutive bins per lane
+// (their bytes as aligned 32-bit words: 32 bytes at D = 2), so 64 / (B / 16)
+// envs share a wave (16 at 64 bins).  With one lane per (env, bin) the step
+// was issue-bound, not HBM-bound: every lane of an env draws the env's item
 // (two engine draws and a double-precision canonical, register-only) and
 // steps its stream with 64-bit modular multiplies, so the instruction count
-// per byte falls with the bins a lane carries (round 6: one env per wave at
-// 64 bins gave 1.27 TB/s at 1M envs with the traffic at its algorithmic
-// bytes, counters: 25% issuing, 40% issue stalls, 35% waiting on memory).
+// per byte falls with the bins a lane carries.  Round 6, 64 bins, 2-D, 1M
+// envs: one env per wave 1.27 TB/s with the traffic at its algorithmic bytes
+// (counters: 25% issuing, 40% issue stalls, 35% waiting on memory); 4 / 8 /
+// 16 / 32 / 64 bins per lane 2.7 / 3.9 / 4.8 / 5.3 / 4.8 TB/s; at 32768 envs
+// (launch-bound) 16 is the fastest (tools/env_ab.sh, profiles/r06j-k_*).
+#ifndef XH_VENV_BPL
+#define XH_VENV_BPL 16
+#endif
 template <int B, int D>
 struct VStepShape {
-  static constexpr int BPL = 4;            // bins per lane (contiguous)
+  // bins per lane (contiguous; at most B)
+  static constexpr int BPL = XH_VENV_BPL < B ? XH_VENV_BPL : B;
+  static constexpr int NW = BPL * D / 4;   // 32-bit words per lane
+  // the lane's words' alignment (the env row starts at env * B * D)
+  static constexpr int LOWBIT = (4 * NW) & -(4 * NW);
+  static constexpr int ALIGN = LOWBIT > 16 ? 16 : LOWBIT;
   static constexpr int LPE = B / BPL;      // lanes per env
   static constexpr int EPW = 64 / LPE;     // envs per wave
   static constexpr int BD = B * D;
@@ -95,11 +106,13 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   const bool masked_in = !a.mask || a.mask[ec];
   const unsigned itw = *reinterpret_cast<const unsigned *>(ip);
   uint32_t x = a.rng[ec];
-  // this lane's bins li * 4 .. li * 4 + 3: D words, byte k * D + d = bin k, dim d
-  uint32_t wv[D];
+  // this lane's bins li BPL .. li BPL + BPL - 1: NW words, byte k D + d =
+  // bin k, dim d
+  const uint32_t *wp = reinterpret_cast<const uint32_t *>(
+      __builtin_assume_aligned(bp + li * S::BPL * D, S::ALIGN));
+  uint32_t wv[S::NW];
 #pragma unroll
-  for (int q = 0; q < D; ++q)
-    wv[q] = reinterpret_cast<const uint32_t *>(bp + li * S::BPL * D)[q];
+  for (int q = 0; q < S::NW; ++q) wv[q] = wp[q];
   int v[S::BPL][D];
 #pragma unroll
   for (int k = 0; k < S::BPL; ++k)
@@ -146,9 +159,9 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
   if (a.mode == 1) x = mstd_mulmod(x, a.skip_mul);  // the policy's draws
   const bool reset = a.mode == 1 && over;
   {
-    uint32_t ow[D];
+    uint32_t ow[S::NW];
 #pragma unroll
-    for (int q = 0; q < D; ++q) ow[q] = 0u;
+    for (int q = 0; q < S::NW; ++q) ow[q] = 0u;
 #pragma unroll
     for (int k = 0; k < S::BPL; ++k)
 #pragma unroll
@@ -156,9 +169,10 @@ __global__ __launch_bounds__(256) void venv_step_kernel(VenvArgs a) {
         const int j = k * D + d;
         ow[j >> 2] |= (uint32_t)((reset ? kCapacity : nb[k][d]) & 0xff) << (8 * (j & 3));
       }
+    uint32_t *op = reinterpret_cast<uint32_t *>(
+        __builtin_assume_aligned(bp + li * S::BPL * D, S::ALIGN));
 #pragma unroll
-    for (int q = 0; q < D; ++q)
-      reinterpret_cast<uint32_t *>(bp + li * S::BPL * D)[q] = ow[q];
+    for (int q = 0; q < S::NW; ++q) op[q] = ow[q];
   }
   // every lane of the env draws the same item (redundant, register-only: no
   // cross-lane hand-off of the new item); the bin-0 lane writes the record
@@ -266,7 +280,7 @@ static dim3 venv_grid(int N, int B) {
 }
 // the step kernel's (VStepShape: 4 bins per lane)
 static dim3 venv_step_grid(int N, int B) {
-  const int epw = 64 / (B / 4);
+  const int epw = 64 / (B / (XH_VENV_BPL < B ? XH_VENV_BPL : B));
   const long waves = (N + epw - 1) / epw;
   return dim3((unsigned)((waves + 3) / 4));
 }
