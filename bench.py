@@ -203,7 +203,7 @@ def library_sha256():
 
 
 def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None,
-                meta_match=None):
+                meta_match=None, envs=None):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 FETCH_SIZE /
     WRITE_SIZE summary (separate --pmc passes; tools/pmc_summary.py):
     2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read correction measured for 1- to
@@ -225,6 +225,10 @@ def pmc_traffic(kernel="policy_train", any_shape=False, lib_sha=None,
         if lib_sha is None or meta.get("library_sha256") != lib_sha:
             continue
         if meta_match and any(meta.get(k) != v for k, v in meta_match.items()):
+            continue
+        # a summary that records its run's env count (tools/gpu_profile_env.sh)
+        # counts only for that count: bytes per launch scale with it
+        if envs is not None and meta.get("envs", envs) != envs:
             continue
         # keys are short kernel names (policy_train_kernel, policy_train8_kernel)
         s = next((v for k, v in sorted(summ.items())
@@ -664,8 +668,8 @@ def main():
     # name; the f32 kernels by their PShape<B, D, H1, H2> instantiation
     lib_sha = library_sha256()
     traffic, traffic_src, pmc = (
-        pmc_traffic(kt["kernel"], any_shape=True, lib_sha=lib_sha) if split
-        else pmc_traffic(lib_sha=lib_sha))
+        pmc_traffic(kt["kernel"], any_shape=True, lib_sha=lib_sha, envs=n) if split
+        else pmc_traffic(lib_sha=lib_sha, envs=n))
     if args.rollout_steps and args.rollout_steps != cfg["T"]:
         # the PMC passes profile the config's own T: their bytes per launch
         # are not this launch's

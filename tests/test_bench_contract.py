@@ -110,3 +110,27 @@ def test_bench_refuses_kernel_overrides(var):
                          capture_output=True, text=True, env=env, timeout=60)
     assert out.returncode == 2 and var in out.stderr, (out.returncode, out.stderr)
     assert out.stdout.strip() == ""
+
+
+def test_pmc_traffic_skips_another_env_count(bench, tmp_path, monkeypatch):
+    """A summary that records its run's env count (the env-only and 1M-env
+    trainer profiles) is cited only for that count: the 1M-env profile of
+    the config-3 train kernel must not give the 32768-env line its bytes."""
+    import json
+    bench.select_config(3)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    k = "policy_train_spec8_kernel"
+    for name, meta, b in (("r99a_c3", {}, 5.0),
+                          ("r99b_c3_env1m", {"envs": 1048576,
+                                             "workload": "config3_trainer"}, 9.0)):
+        m = dict(meta, library_sha256="f" * 64, created="2026-01-0%dT00:00:00+00:00"
+                 % (1 if b == 5.0 else 2))
+        summ = {k: {"kernel": "xh::sp8::" + k + "(xh::PolicyTrainArgs)", "hbm_bytes": b},
+                "_meta": m}
+        (prof / ("%s_pmc_summary.json" % name)).write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    t, src, _ = bench.pmc_traffic(k, any_shape=True, lib_sha="f" * 64, envs=32768)
+    assert t == 5.0 and src == "profiles/r99a_c3_pmc_summary.json"
+    t, _, _ = bench.pmc_traffic(k, any_shape=True, lib_sha="f" * 64, envs=1048576)
+    assert t == 9.0

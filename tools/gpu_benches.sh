@@ -18,4 +18,8 @@ for c in 3 2 5; do
   timeout -k 10 300 python -u bench.py --config $c --algo klppo --steps 5 --warmup 1 > $O/bkl$c.log 2>&1 || { tail -5 $O/bkl$c.log; exit 1; }
   tail -1 $O/bkl$c.log > $O/profiles/${TAG}_bench_config${c}_klppo.json
 done
+timeout -k 10 120 python -u bench.py --env-only --steps 20 --warmup 2 > $O/benv.log 2>&1 || { tail -5 $O/benv.log; exit 1; }
+tail -1 $O/benv.log > $O/profiles/${TAG}_bench_envonly.json
+timeout -k 10 120 python -u bench.py --env-only --envs 1048576 --steps 20 --warmup 2 --no-cpu-baseline > $O/benv1m.log 2>&1 || { tail -5 $O/benv1m.log; exit 1; }
+tail -1 $O/benv1m.log > $O/profiles/${TAG}_bench_envonly_1m.json
 cut -c1-200 $O/profiles/${TAG}_bench_config*.json
