@@ -108,15 +108,16 @@ __global__ __launch_bounds__(kELB) void end_write_kernel(EndListArgs a,
 // The same list in one launch of one workgroup for N <= 1024 C, N % 4 == 0
 // (used up to C = 8):
 // thread i owns envs [i C, (i+1) C), reads their done bytes as 32-bit words
-// (independent loads), keeps one count per env in registers, one block-wide
-// exclusive scan of the thread totals, then writes its envs' entries (t outer,
-// so each env's entries stay in t order at their env-major positions).
+// (independent loads), keeps one count per env in registers; the exclusive
+// scan of the thread totals is a wave scan (shuffles) plus the sixteen wave
+// totals from LDS behind one barrier (integer sums: any order is exact); then
+// each thread writes its envs' entries (t outer, so each env's entries stay
+// in t order at their env-major positions).
 template <int C>
 __global__ __launch_bounds__(1024) void end_list_kernel(EndListArgs a) {
   static_assert(C % 4 == 0, "whole words");
-  __shared__ int sc[1024];
-  __shared__ int osum[1024];
-  const int tid = threadIdx.x, e0 = tid * C;
+  __shared__ int wsum[16], wopen[16];
+  const int tid = threadIdx.x, e0 = tid * C, wv = tid >> 6, ln = tid & 63;
   int cnt[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) cnt[i] = 0;
@@ -143,22 +144,23 @@ __global__ __launch_bounds__(1024) void end_list_kernel(EndListArgs a) {
   int total = 0;
 #pragma unroll
   for (int i = 0; i < C; ++i) total += cnt[i];
-  sc[tid] = total;
-  osum[tid] = open;
+  int incl = total;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(incl, d, 64);
+    if (ln >= d) incl += u;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) open += __shfl_xor(open, d, 64);
+  if (ln == 63) wsum[wv] = incl;
+  if (ln == 0) wopen[wv] = open;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int u = tid >= off ? sc[tid - off] : 0;
-    __syncthreads();
-    sc[tid] += u;
-    __syncthreads();
-  }
-  for (int off = 512; off > 0; off >>= 1) {
-    if (tid < off) osum[tid] += osum[tid + off];
-    __syncthreads();
-  }
+  int base = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) base += i < wv ? wsum[i] : 0;
   int pos[C];
   {
-    int p = sc[tid] - total;
+    int p = base + incl - total;
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       pos[i] = p;
@@ -174,9 +176,15 @@ __global__ __launch_bounds__(1024) void end_list_kernel(EndListArgs a) {
         if ((v >> (8 * b)) & 0xffu) a.end_list[pos[4 * w + b]++] = t * a.N + e0 + 4 * w + b;
     }
   if (tid == 0) {
-    *a.n_end = sc[1023];
-    *a.n_open = osum[0];
-    if (a.rows_out) *a.rows_out = a.rows_base + sc[1023];
+    int ne = 0, no = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ne += wsum[i];
+      no += wopen[i];
+    }
+    *a.n_end = ne;
+    *a.n_open = no;
+    if (a.rows_out) *a.rows_out = a.rows_base + ne;
   }
 }
 

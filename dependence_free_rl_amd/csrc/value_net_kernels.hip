@@ -104,12 +104,11 @@ __device__ __forceinline__ float item_sum_tree(const float *col, int D, int B) {
   const float s = (r[0] + r[1]) + (r[2] + r[3]);
   return (s + 0.0f) + (0.0f + 0.0f);
 }
-// isum == nullptr (B <= 64): the item sums computed here (one launch fewer)
-__global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B, int D,
-                               int nkb, bf16x8 *frag) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * nkb * 64) return;
-  const int lane = i & 63, kb = (i >> 6) % nkb, cb = (i >> 6) / nkb;
+// The three parts of fragment (cb, kb) of one lane (isum == nullptr, B <=
+// 64: the item sums computed here)
+__device__ __forceinline__ void w0_frag_parts(const float *W0, const float *isum, int in,
+                                              int B, int D, int cb, int kb, int lane,
+                                              bf16x8 (&out)[3]) {
   const int n = 32 * cb + (lane & 31), k0 = 16 * kb + 8 * (lane >> 5);
   const int BD = B * D, K = BD + D;
   const float *Wn = W0 + (size_t)n * in;
@@ -124,13 +123,24 @@ __global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B
       w = isum ? isum[n * D + (k - BD)] : item_sum_tree(Wn + D + (k - BD), D, B);
     split3(w * (1.0f / (float)kCapacity), hi[j], mid[j], lo[j]);
   }
+  out[0] = __builtin_bit_cast(bf16x8, u32x4{pk(hi[0], hi[1]), pk(hi[2], hi[3]),
+                                            pk(hi[4], hi[5]), pk(hi[6], hi[7])});
+  out[1] = __builtin_bit_cast(bf16x8, u32x4{pk(mid[0], mid[1]), pk(mid[2], mid[3]),
+                                            pk(mid[4], mid[5]), pk(mid[6], mid[7])});
+  out[2] = __builtin_bit_cast(bf16x8, u32x4{pk(lo[0], lo[1]), pk(lo[2], lo[3]),
+                                            pk(lo[4], lo[5]), pk(lo[6], lo[7])});
+}
+__global__ void w0_frag_kernel(const float *W0, const float *isum, int in, int B, int D,
+                               int nkb, bf16x8 *frag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * nkb * 64) return;
+  const int lane = i & 63, kb = (i >> 6) % nkb, cb = (i >> 6) / nkb;
+  bf16x8 v[3];
+  w0_frag_parts(W0, isum, in, B, D, cb, kb, lane, v);
   const size_t f = ((size_t)cb * nkb + kb) * 64 + lane, ps = (size_t)2 * nkb * 64;
-  frag[f] = __builtin_bit_cast(bf16x8, u32x4{pk(hi[0], hi[1]), pk(hi[2], hi[3]),
-                                             pk(hi[4], hi[5]), pk(hi[6], hi[7])});
-  frag[f + ps] = __builtin_bit_cast(bf16x8, u32x4{pk(mid[0], mid[1]), pk(mid[2], mid[3]),
-                                                  pk(mid[4], mid[5]), pk(mid[6], mid[7])});
-  frag[f + 2 * ps] = __builtin_bit_cast(bf16x8, u32x4{pk(lo[0], lo[1]), pk(lo[2], lo[3]),
-                                                      pk(lo[4], lo[5]), pk(lo[6], lo[7])});
+  frag[f] = v[0];
+  frag[f + ps] = v[1];
+  frag[f + 2 * ps] = v[2];
 }
 
 // ---------------------------------------------------------------- forward --
@@ -146,6 +156,12 @@ struct FwdArgs {
   int max_rows;
   const bf16x8 *w0f;
   int nkb;
+  // w0src != nullptr (up to 64 bins, fresh parameters): every wave splits its
+  // own fragments from W0 (w0_frag_kernel's values, its launch saved) and
+  // workgroup 0 stores them to w0f_out for the next forward
+  const float *w0src;
+  bf16x8 *w0f_out;
+  int in, B;
   const float *b0, *W1, *b1, *W2, *b2;
   float *act0, *act1;  // layer outputs of rows < act_rows (the backward's)
   int act_rows;
@@ -185,7 +201,9 @@ __device__ __forceinline__ int fwd_idx(const FwdArgs &o, int m, int &sub) {
 // 16w..16w+15) and layer 2 (a 16-lane DPP sum) from the H1 tile in LDS.
 // Per tile: K loop | barrier | stage tile + 1, load tile + 2 | H1 | barrier |
 // layers 1, 2.
-template <int NKH>  // >= k blocks per half
+// SPLIT: the W0 split inside (o.w0src; instantiated up to NKH 3 -- beyond, the
+// item sums' unrolled loads spill the kernel)
+template <int NKH, bool SPLIT>  // >= k blocks per half
 __global__ __launch_bounds__(256, 1) void vnet_forward_kernel(FwdArgs o) {
   constexpr int XP = 32 * NKH + 8;          // bf16 row stride (848 B at NKH 13)
   constexpr int NCH = (2 * NKH + 3) / 4;    // 16-byte chunks per thread and tile
@@ -195,23 +213,45 @@ __global__ __launch_bounds__(256, 1) void vnet_forward_kernel(FwdArgs o) {
   __shared__ __attribute__((aligned(16))) float w1s[V2][V1 + 4];
   const int M = o.rows ? min(o.max_rows, *o.rows) : o.max_rows;
   const int ntiles = (M + TM - 1) / TM;
-  if ((int)blockIdx.x >= ntiles) return;  // uniform
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l31 = lane & 31, h = lane >> 5, l15 = lane & 15, q = lane >> 4;
   const int cb = w & 1, kh = w >> 1;
   const int nkb = 2 * NKH, kbase = NKH * kh;  // o.nkb == 2 NKH (zero-padded)
   const int BD = o.BD, D = o.D, K = BD + D, ncpr = BD / 16;
+  bf16x8 wf[NKH][3];
+  const size_t ps = (size_t)2 * nkb * 64;
+  // the fragments from W0; workgroup 0 stores them (with or without a tile)
+  auto split_w0 = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < NKH; ++kb)
+      w0_frag_parts(o.w0src, nullptr, o.in, o.B, D, cb, kbase + kb, lane, wf[kb]);
+    if (blockIdx.x == 0) {
+#pragma unroll
+      for (int kb = 0; kb < NKH; ++kb) {
+        const size_t f = ((size_t)cb * nkb + kbase + kb) * 64 + lane;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) o.w0f_out[f + p * ps] = wf[kb][p];
+      }
+    }
+  };
+  if ((int)blockIdx.x >= ntiles) {  // uniform
+    if constexpr (SPLIT)
+      if (blockIdx.x == 0) split_w0();
+    return;
+  }
   for (int i = tid; i < V2 * V1; i += 256) w1s[i / V1][i % V1] = o.W1[i];
   // features K .. 16 nkb - 1 meet zero weights: finite zeros, once
   for (int i = tid; i < TM * (16 * nkb - K); i += 256)
     xs[i / (16 * nkb - K)][K + i % (16 * nkb - K)] = (__bf16)0.0f;
-  bf16x8 wf[NKH][3];
-  const size_t ps = (size_t)2 * nkb * 64;
+  if constexpr (SPLIT) {
+    split_w0();
+  } else {
 #pragma unroll
-  for (int kb = 0; kb < NKH; ++kb) {
-    const size_t f = ((size_t)cb * nkb + kbase + kb) * 64 + lane;
+    for (int kb = 0; kb < NKH; ++kb) {
+      const size_t f = ((size_t)cb * nkb + kbase + kb) * 64 + lane;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) wf[kb][p] = o.w0f[f + p * ps];
+      for (int p = 0; p < 3; ++p) wf[kb][p] = o.w0f[f + p * ps];
+    }
   }
   const float bias0 = o.b0[32 * cb + l31];
   const float b1a = o.b1[l15], b1b = o.b1[16 + l15];
@@ -664,15 +704,19 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   const int in = a.w[0];
   bf16x8 *frag = (bf16x8 *)a.w0frag;
   float *isum = (float *)((char *)a.w0frag + vnet_frag_only(a.env));
-  // up to 64 bins the fragment kernel sums the item columns itself (config 2:
-  // one 4-us launch fewer per forward); at 128 the serial sums cost more
-  // (XH_W0_FUSE=0: always the separate item kernel; tests compare the two)
-  static const bool fuse_ok = [] {
+  // up to 64 bins the forward splits W0 itself, item sums included (config
+  // 2: two launches fewer per forward than the item kernel + the fragment
+  // kernel); at 128 bins the serial sums cost more.  XH_W0_FUSE=0: the item
+  // kernel and the fragment kernel; =1: the fragment kernel with the item
+  // sums (tests compare the three)
+  static const int fuse_mode = [] {
     const char *e = std::getenv("XH_W0_FUSE");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
   }();
-  const bool fuse = fuse_ok && a.env.B <= 64;
-  if (!a.w0frag_ready) {
+  const bool fuse = fuse_mode >= 1 && a.env.B <= 64;
+  const bool in_fwd = fuse_mode == 2 && a.env.B <= 64 && vnet_nkh(a.env) <= 3 &&
+                      !a.w0frag_ready;
+  if (!a.w0frag_ready && !in_fwd) {
     if (!fuse)
       hipLaunchKernelGGL(w0_item_kernel, dim3(V1 * a.env.D), dim3(256), 0, s, a.params, in,
                          a.env.B, a.env.D, isum);
@@ -695,6 +739,10 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   o.max_rows = a.max_rows;
   o.w0f = frag;
   o.nkb = nkb;
+  o.w0src = in_fwd ? a.params : nullptr;
+  o.w0f_out = frag;
+  o.in = in;
+  o.B = a.env.B;
   o.b0 = a.params + (size_t)V1 * in;
   o.W1 = a.params + o1;
   o.b1 = a.params + o1 + V2 * V1;
@@ -715,7 +763,13 @@ hipError_t vnet_forward(const MlpArgs &a, hipStream_t s) {
   switch (vnet_nkh(a.env)) {
 #define XH_VNET_FWD(n)                                                          \
   case n:                                                                       \
-    hipLaunchKernelGGL(vnet_forward_kernel<n>, grid, dim3(256), 0, s, o);       \
+    if constexpr (n <= 3) {                                                     \
+      if (in_fwd) {                                                             \
+        hipLaunchKernelGGL((vnet_forward_kernel<n, true>), grid, dim3(256), 0, s, o); \
+        break;                                                                  \
+      }                                                                         \
+    }                                                                           \
+    hipLaunchKernelGGL((vnet_forward_kernel<n, false>), grid, dim3(256), 0, s, o); \
     break;
     XH_VNET_FWD(1) XH_VNET_FWD(2) XH_VNET_FWD(3) XH_VNET_FWD(4) XH_VNET_FWD(5)
     XH_VNET_FWD(6) XH_VNET_FWD(8) XH_VNET_FWD(10) XH_VNET_FWD(13)

@@ -60,12 +60,17 @@ def test_value_kernels_against_gemm(ctx, monkeypatch, algo, B, D, widths, N, T):
     got, kg = run(None)
     assert (kr, km, kg) == ("gemm", "mlp3_fused", "vnet_bf16")
     if B <= 64:
-        # the W0 fragments' item sums inside w0_frag_kernel (the default up
-        # to 64 bins) have the bits of the separate w0_item_kernel
+        # the W0 fragments split inside the forward (the default up to 64 bins
+        # and 3 k blocks per half) and by w0_frag_kernel with its own item
+        # sums (XH_W0_FUSE=1) have the bits of w0_item_kernel +
+        # w0_frag_kernel (XH_W0_FUSE=0)
         sep, _ = run(None, w0_fuse="0")
-        for it, (x, y) in enumerate(zip(got, sep)):
-            for i, (a, b) in enumerate(zip(x, y)):
-                np.testing.assert_array_equal(a, b, err_msg="w0 fuse iteration %d item %d" % (it, i))
+        frk, _ = run(None, w0_fuse="1")
+        for mode, other in (("default", got), ("1", frk)):
+            for it, (x, y) in enumerate(zip(other, sep)):
+                for i, (a, b) in enumerate(zip(x, y)):
+                    np.testing.assert_array_equal(
+                        a, b, err_msg="w0 mode %s iteration %d item %d" % (mode, it, i))
     worst = {}
     for it, (x, y, z) in enumerate(zip(got, ref, m3)):
         for i, (a, b, c) in enumerate(zip(x, y, z)):
