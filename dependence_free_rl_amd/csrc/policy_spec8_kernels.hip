@@ -106,6 +106,11 @@
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
 #endif
+// XH_SP8_NODW3 (timing-study builds only, wrong results): 1 drops the
+// per-group dW3 FMAs from the matrix waves' slots, 2 the dW3 and db2 sums
+#ifndef XH_SP8_NODW3
+#define XH_SP8_NODW3 0
+#endif
 // XH_SP8_DHI / XH_SP8_L2I (A/B builds): dH1's (vector) / layer 2's (matrix)
 // 16 steps in the order (t = st & 1, ks = st >> 1), alternating the two
 // r-tiles' accumulators, instead of all of r-tile 0's steps first (a
@@ -708,9 +713,10 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // dW3 / db2 sums of layer-2 value e of r-tile t (units of S2; w3 at the
     // write-out)
     auto dw3_e = [&](const f32x16s (&c)[2], int t, int e) {
+      if (XH_SP8_NODW3 >= 2) return;
       const float v = c[t][e];
       const float gm = v > 0.0f ? gz[t] : 0.0f;
-      acc3[e] = fmaf(gm, v, acc3[e]);
+      if (XH_SP8_NODW3 == 0) acc3[e] = fmaf(gm, v, acc3[e]);
       accb2[e] += gm;
     };
     // relu masks of block (t, q) as 0 / 0x4000 -> slot ms: 0x4000 is 2.0 both
