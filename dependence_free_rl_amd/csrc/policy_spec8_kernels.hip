@@ -106,11 +106,6 @@
 #ifndef XH_SP8_GH2
 #define XH_SP8_GH2 0
 #endif
-// XH_SP8_NODW3 (timing-study builds only, wrong results): 1 drops the
-// per-group dW3 FMAs from the matrix waves' slots, 2 the dW3 and db2 sums
-#ifndef XH_SP8_NODW3
-#define XH_SP8_NODW3 0
-#endif
 // XH_SP8_DHI / XH_SP8_L2I (A/B builds): dH1's (vector) / layer 2's (matrix)
 // 16 steps in the order (t = st & 1, ks = st >> 1), alternating the two
 // r-tiles' accumulators, instead of all of r-tile 0's steps first (a
@@ -386,9 +381,9 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int e = 0; e < 16; ++e) accW2[mt][e] = 0.0f;
-    float acc3[16], accb2[16];
+    float accb2[16];  // db2 sums, 2 g M (the f16 mask 2.0)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc3[e] = accb2[e] = 0.0f;
+    for (int e = 0; e < 16; ++e) accb2[e] = 0.0f;
     if (s == 0 && h == 0) lf[F_DB3 + l31] = 0.0f;
 
     struct Raw {
@@ -710,27 +705,26 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
           if (!acc) gz[0] = gz[1] = 0.0f;
       }
     };
-    // dW3 / db2 sums of layer-2 value e of r-tile t (units of S2; w3 at the
-    // write-out)
-    auto dw3_e = [&](const f32x16s (&c)[2], int t, int e) {
-      if (XH_SP8_NODW3 >= 2) return;
-      const float v = c[t][e];
-      const float gm = v > 0.0f ? gz[t] : 0.0f;
-      if (XH_SP8_NODW3 == 0) acc3[e] = fmaf(gm, v, acc3[e]);
-      accb2[e] += gm;
-    };
-    // relu masks of block (t, q) as 0 / 0x4000 -> slot ms: 0x4000 is 2.0 both
-    // as bf16 (dW2's A operand) and as f16 (dH1's), so one image serves both
-    // MFMA types (the factor 2 is taken back exactly at the write-outs)
-    auto mask_q = [&](const f32x16s (&c)[2], int ms, int t, int q) {
+    // the relu mask of layer-2 value e of r-tile t as 0 / 0x4000 (2.0 both
+    // as bf16, dW2's A operand, and as f16, dH1's: one image serves both MFMA
+    // types, the factor 2 taken back exactly at the write-outs); db2's sum
+    // 2 g M by one v_fma_mix_f32 reading the word's low half as f16; the
+    // words of block (t, q) stored into slot ms after its fourth value.  dW3
+    // needs no per-row work: it is reassociated through dW2 after the loop.
+    unsigned mwd[4];
+    auto mv_e = [&](const f32x16s (&c)[2], int ms, int t, int e) {
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-      const int mb = 2 * kImg * ms;  // (mwb holds L_MK)
-      unsigned m[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) m[u] = c[t][4 * q + u] > 0.0f ? 1u : 0u;
-      const u32x2 mm = {(unsigned)__umul24(m[0] | (m[1] << 16), 0x4000u),
-                        (unsigned)__umul24(m[2] | (m[3] << 16), 0x4000u)};
-      st4(mb + 8192 * t + mwb[q], __builtin_bit_cast(bf16x4, mm));
+      const int q = e >> 2, u = e & 3;
+      const unsigned wv = c[t][e] > 0.0f ? 0x4000u : 0u;
+      float acc = accb2[e];
+      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(wv), "v"(gz[t]));
+      accb2[e] = acc;
+      mwd[u] = wv;
+      if (u == 3) {
+        const int mb = 2 * kImg * ms;  // (mwb holds L_MK)
+        const u32x2 mm = {mwd[0] | (mwd[1] << 16), mwd[2] | (mwd[3] << 16)};
+        st4(mb + 8192 * t + mwb[q], __builtin_bit_cast(bf16x4, mm));
+      }
     };
     // dW2 += M^T (S_H g (x) H1) of the group whose masks are in slot ms:
     // 16 steps (K-step ks = st / 4 of 16 rows, o-tile mt = st % 4) of three
@@ -774,17 +768,15 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       }
     };
     // B's VALU in dW2's 48 slots: the softmax stages (loads in slot 0, the
-    // arithmetic from slot 3 on, one stage per slot), then group gi's dW3 /
-    // db2 sums (slots 12 .. 43) with its mask blocks every fourth slot from 15
+    // arithmetic from slot 3 on, one stage per slot), then group gi's masks
+    // and db2 sums (slots 12 .. 43), a mask block stored every fourth slot
     auto b_task = [&](const f32x16s (&c)[2], int gi, int gpar, bool acc, int k) {
       if (k == 0)
         softmax_stage(gi, gpar, acc, 0);
       else if (k >= 3 && k < (XH_SP8_KL_TU ? 10 : 9))
         softmax_stage(gi, gpar, acc, k - 2);
-      else if (k >= 12 && k < 44) {
-        dw3_e(c, (k - 12) >> 4, (k - 12) & 15);
-        if ((k & 3) == 3) mask_q(c, gpar, (k - 15) >> 4, ((k - 15) >> 2) & 3);
-      }
+      else if (k >= 12 && k < 44)
+        mv_e(c, gpar, (k - 12) >> 4, (k - 12) & 15);
     };
     auto no_task = [](int) {};
 
@@ -876,17 +868,39 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
         const int o = 32 * mt + 8 * (e >> 2) + 4 * h + (e & 3);
         slab[PL.oW2() + o * kH + 32 * s + l31] = (accW2[mt][e] * rSH) * w3g[o];
       }
+    // dW3 = sum_r g_r relu(A2[r][o]), reassociated through A2 = H1 W2^T + b2:
+    //   dW3[o] = sum_i W2[o][i] G[o][i] + b2[o] D[o],
+    // G = M^T (g (x) H1) (dW2 before its w3 factor), D = M^T g (db2 before
+    // it): no per-row work in the loop.  Its f32 error is of the order of the
+    // rounding of A2 itself.  Each wave's partial sums over
+    // its 32 features i meet in the free g (x) H1 image (one more barrier,
+    // in both roles), summed in a fixed order.
+    float *const d3p = reinterpret_cast<float *>(lds + L_GH);  // [4 s][128 o]
+    float *const d3d = d3p + 4 * kH;                           // [128 o] D
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = 32 * mt + 8 * (e >> 2) + 4 * h + (e & 3);
+        const float sv = seg_sum<32>((accW2[mt][e] * rSH) * P[PL.oW2() + o * kH + 32 * s + l31]);
+        if (l31 == 0) d3p[s * kH + o] = sv;
+      }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      // dW3 / db2 of o = 32 s + 8 (e >> 2) + 4 h + (e & 3): sums over the 32
-      // lanes (rows) of the half
-      const float s3 = seg_sum<32>(acc3[e]);
-      const float s2 = seg_sum<32>(accb2[e]);
+      // db2 of o = 32 s + 8 (e >> 2) + 4 h + (e & 3): sums over the 32 lanes
+      // (rows) of the half
+      const float s2 = seg_sum<32>(accb2[e]) * 0.5f;
       const int o = 32 * s + 8 * (e >> 2) + 4 * h + (e & 3);
       if (l31 == 0) {
-        slab[PL.ow3() + o] = s3 * (1.0f / S2);
+        d3d[o] = s2;
         slab[PL.ob2() + o] = s2 * w3g[o];
       }
+    }
+    __syncthreads();  // the dW3 partials (vector: after their loop)
+    if (h == 0) {
+      const int o = 32 * s + l31;
+      const float si = (d3p[o] + d3p[kH + o]) + (d3p[2 * kH + o] + d3p[3 * kH + o]);
+      slab[PL.ow3() + o] = fmaf(P[PL.ob2() + o], d3d[o], si);
     }
     if (s == 0) {
       const float v3 = seg_sum<32>(lf[F_DB3 + l31]);
@@ -1184,6 +1198,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
 #if XH_SP8_KL_TU
     __syncthreads();  // the matrix waves' KL sum
 #endif
+    __syncthreads();  // the matrix waves' dW3 partials
     // ---- write-out: dW1 / db1 of feature fi (the two lane halves hold row
     // subsets; dH1 was in units of S_D)
     float tw0 = w0 + __shfl_xor(w0, 32, kWave);
