@@ -716,9 +716,7 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
       const int q = e >> 2, u = e & 3;
       const unsigned wv = c[t][e] > 0.0f ? 0x4000u : 0u;
-      float acc = accb2[e];
-      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(wv), "v"(gz[t]));
-      accb2[e] = acc;
+      accb2[e] = fma_mix_lo(wv, gz[t], accb2[e]);
       mwd[u] = wv;
       if (u == 3) {
         const int mb = 2 * kImg * ms;  // (mwb holds L_MK)

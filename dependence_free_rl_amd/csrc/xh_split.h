@@ -262,6 +262,19 @@ __device__ __forceinline__ float f16_scale_for(float m) {
 __device__ __forceinline__ f32x16s mfma_f16(f16x8 a, f16x8 b, f32x16s c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
+// acc + f16(half of w) * g in one v_fma_mix_f32 (the f16 operand read from the
+// low / high half of w): a relu-mask word's 0 / 0x4000 (2.0) half times g,
+// i.e. db2's masked sum 2 g M without a compare or a select
+__device__ __forceinline__ float fma_mix_lo(unsigned w, float g, float acc) {
+  asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(w), "v"(g));
+  return acc;
+}
+__device__ __forceinline__ float fma_mix_hi(unsigned w, float g, float acc) {
+  asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "+v"(acc)
+      : "v"(w), "v"(g));
+  return acc;
+}
 // the bits of a bf16 0/1 operand as f16 (1.0 = 0x3F80 -> 0x3C00)
 __device__ __forceinline__ f16x8 mask_bf16_to_f16(bf16x8 m) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
