@@ -711,16 +711,24 @@ __global__ __launch_bounds__(kThreads, 2) void policy_train_spec8_kernel(PolicyT
     // 2 g M by one v_fma_mix_f32 reading the word's low half as f16; the
     // words of block (t, q) stored into slot ms after its fourth value.  dW3
     // needs no per-row work: it is reassociated through dW2 after the loop.
-    unsigned mwd[4];
+    unsigned mwd[2];
     auto mv_e = [&](const f32x16s (&c)[2], int ms, int t, int e) {
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
       const int q = e >> 2, u = e & 3;
-      const unsigned wv = c[t][e] > 0.0f ? 0x4000u : 0u;
-      accb2[e] = fma_mix_lo(wv, gz[t], accb2[e]);
-      mwd[u] = wv;
+      if ((u & 1) == 0) {
+        // the pair's word: relu'(x) in {0, 1} from x's bits by v_med3_i32 (no
+        // compare writing VCC), packed and times 0x4000 by the 24-bit multiply
+        int m0, m1;
+        asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m0) : "v"(__float_as_int(c[t][e])));
+        asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m1) : "v"(__float_as_int(c[t][e + 1])));
+        mwd[u >> 1] = (unsigned)__umul24((unsigned)m0 | ((unsigned)m1 << 16), 0x4000u);
+        accb2[e] = fma_mix_lo(mwd[u >> 1], gz[t], accb2[e]);
+      } else {
+        accb2[e] = fma_mix_hi(mwd[u >> 1], gz[t], accb2[e]);
+      }
       if (u == 3) {
         const int mb = 2 * kImg * ms;  // (mwb holds L_MK)
-        const u32x2 mm = {mwd[0] | (mwd[1] << 16), mwd[2] | (mwd[3] << 16)};
+        const u32x2 mm = {mwd[0], mwd[1]};
         st4(mb + 8192 * t + mwb[q], __builtin_bit_cast(bf16x4, mm));
       }
     };
